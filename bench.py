@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Benchmark: trajectories/s of the batched 10-segment N=10 3-D minimum-snap solve.
+
+Workload (BASELINE.json configs[1], "config 2"): per GPU a batch of B = 1e4
+trajectories from the reference bench generator
+createRandomVerticesPath(3, 10, 5.0, SNAP, seed) + estimateSegmentTimes(2, 2, 6.5)
+(src/polynomial_timing_evaluation.cpp:34-112), seeds rank*B .. rank*B+B-1 (so
+at N = 8 with --batch 125000 this is exactly config 3's 1e6 sharded batch).
+One step = one batched setupFromVertices + solveLinear of the whole batch
+(fused HIP kernel, inputs already resident in HBM, coefficients written to HBM).
+
+Multi-GPU: one process per GPU (torchrun), contiguous shards, no data-path
+collective ("scaling": "weak"); a barrier + MAX-over-ranks of the timed region.
+
+Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline
+(algorithmic bytes / measured kernel time vs 8 TB/s HBM peak) and the CPU
+baseline (the oracle restatement of the reference algorithm on host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes_per_traj(N, D, K):
+    """Bytes the ABI must move per trajectory: values [V][h][D] f64 + mask [V] u8
+    + times [K] f64 in, coefficients [K][D][N] f64 out.  Config 2: 1411 + 2400 = 3811 B."""
+    V, h = K + 1, N // 2
+    return V * h * D * 8 + V + K * 8 + K * D * N * 8
+
+
+def traffic_from_profiles(kernel_prefix, batch):
+    """HBM bytes per launch of the solve kernel from the committed PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        ent = d.get(kernel_prefix, {}).get(str(batch))
+        return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(values, mask, times, N, r, target_s, threads):
+    """Oracle (faithful C restatement of lin_impl, dense QR in place of SparseQR) on host cores."""
+    from oracle import pyoracle
+    lib = pyoracle.build(build_dir="_build_bench", arch=os.environ.get("MTG_ORACLE_ARCH", "native"))
+    pyoracle._LIB = None
+    pyoracle.lib(lib)  # the copy built on this host with -march=native
+    m32 = mask.astype(np.uint32)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        pyoracle.solve_linear_batch(N, r, values, m32, times, threads=threads)
+        done += len(values)
+        el = time.perf_counter() - t0
+        if el >= target_s:
+            break
+    return done / el, el, done
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (config 2: 1e4)")
+    ap.add_argument("--segments", type=int, default=10)
+    ap.add_argument("--N", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample", type=int, default=20000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", action="store_true", help="two-kernel path (assembly + block Cholesky)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import mav_trajectory_generation_cmake_amd as mtg
+
+    N, K, D, r = args.N, args.segments, 3, 4
+    B = args.batch
+    values, mask, times = mtg.random_vertices_path_batch(N, D, K, B, seed0=rank * B)
+    v_d = torch.from_numpy(values).to(dev)
+    m_d = torch.from_numpy(mask).to(dev)
+    t_d = torch.from_numpy(times).to(dev)
+    c_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
+    ctx = mtg.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+
+    def step():
+        ctx.solve_linear_batch(N, r, v_d, m_d, t_d, coeffs=c_d, split=args.split, asynchronous=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    el = float(tmax.item())
+
+    # spot check of the timed outputs (finite, constraint continuity) -- not timed
+    c = c_d.cpu().numpy()
+    assert np.isfinite(c).all(), "non-finite coefficients"
+
+    total = B * world * args.steps
+    value = total / el
+    bpt = algorithmic_bytes_per_traj(N, D, K)
+    achieved = bpt * B / (kern_ms * 1e-3) / 1e9
+    traffic = traffic_from_profiles("solve_fused_kernel", B)
+    out = {
+        "metric": "trajectories/sec (10-seg, N=10, 3-D min-snap) at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "trajectories/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: reference bench generator createRandomVerticesPath(3,10,5.0,SNAP,seed) "
+                "+ estimateSegmentTimes(2,2,6.5), seeds rank*B..rank*B+B-1",
+        "config": {"workload": "config2: %d x (K=%d, N=%d, D=%d, r=SNAP) per GPU, device-resident" % (B, K, N, D),
+                   "batch_per_gpu": B, "global_batch": B * world, "segments": K, "N": N, "D": D,
+                   "derivative_to_optimize": r, "parallelism": "shard%d" % world,
+                   "kernel_path": "split" if args.split else "fused"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "kernel": "solve_fused_kernel<10>" if not args.split else "assemble+block_cholesky",
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_traj": bpt},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("MTG_CPU_THREADS", min(16, os.cpu_count() or 1)))
+        S = min(args.cpu_sample, B)
+        rate, cel, done = cpu_baseline(values[:S], mask[:S], times[:S], N, r, args.cpu_seconds, threads)
+        out["cpu_baseline"] = {"value": rate, "unit": "trajectories/s", "cores": threads, "kind": "port",
+                               "sample": "%d trajectories of this rank's shard, solved repeatedly for %.1f s "
+                                         "(%d solves) by the oracle restatement (-O3 -march=native, OpenMP)"
+                                         % (S, cel, done)}
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

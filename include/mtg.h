@@ -1,0 +1,158 @@
+/*
+ * mtg.h -- C ABI of the MI355X batched minimum-derivative polynomial
+ * optimizer (libmtg.so).  Plain C types only: pointers, sizes, status codes.
+ *
+ * The reference (magrimm/mav_trajectory_generation_cmake) has no FFI; its
+ * boundary is the C++ template class PolynomialOptimization<N>
+ * (mav_trajectory_generation/include/mav_trajectory_generation/
+ * polynomial_optimization_linear.h:45-269).  Each entry point below states
+ * which reference interface it replaces.  The C++ drop-in classes in
+ * include/mav_trajectory_generation/ are written on top of this ABI, and
+ * INTEGRATION.md shows the bindings (C++, ctypes) a maintainer would add.
+ *
+ * Rules: the library never aborts and never throws; calls return MTG_OK or a
+ * negative MTG_ERR_*.  All buffers are caller-owned and never retained after
+ * a call returns (with MTG_FLAG_ASYNC: until the stream is synchronized).
+ * One mtg_ctx serialises its calls; different contexts are thread-safe.
+ *
+ * Data layout (all FP64, row-major, B = batch, V = K + 1 vertices,
+ * h = N / 2 derivatives 0..h-1 per vertex, D dimensions):
+ *   values   [B][V][h][D]  value of derivative k at vertex v, dimension d
+ *                          (read only where the derivative is fixed)
+ *   fixed_mask [B][V]      uint8, bit k set => derivative k of vertex v is
+ *                          fixed (Vertex::addConstraint, vertex.h:58-64);
+ *                          bits >= h are dropped with a warning status, as
+ *                          setupFromVertices does (lin_impl:74-95)
+ *   times    [B][K]        segment times, must be > 0 (lin_impl:287)
+ *   coeffs   [B][K][D][N]  polynomial coefficients, increasing powers
+ *                          (polynomial_optimization_linear.h:42-44)
+ *   free_out [B][D][V*h]   optional: getFreeConstraints() values
+ *                          (polynomial_optimization_linear.h:180-184) in the
+ *                          reference order (sorted by vertex, then derivative)
+ *   n_free_out [B]         optional: getNumberFreeConstraints()
+ *   cost_out [B]           optional: computeCost() = 0.5 sum c^T Q c
+ *                          (lin_impl:114-130)
+ *   status   [B]           optional: per-trajectory MTG_TRAJ_* bits
+ * ("lin_impl" = .../impl/polynomial_optimization_linear_impl.h)
+ */
+#ifndef MTG_H_
+#define MTG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTG_ABI_VERSION 1
+
+/* Call-level return codes. */
+#define MTG_OK 0
+#define MTG_ERR_INVALID_ARGUMENT (-1)
+#define MTG_ERR_UNSUPPORTED_N (-2)     /* N must be even, 2 <= N <= 12 (polynomial.h:46) */
+#define MTG_ERR_BAD_DERIVATIVE (-3)    /* 0 <= r <= N/2-1 (lin_impl:50-55) */
+#define MTG_ERR_SIZE_MISMATCH (-4)     /* K < 1, D < 1, B < 0 (lin_impl:66-67, :279-281) */
+#define MTG_ERR_HIP (-5)               /* HIP runtime error, see mtg_last_error() */
+#define MTG_ERR_NO_DEVICE (-6)
+#define MTG_ERR_OUT_OF_MEMORY (-7)
+#define MTG_ERR_TOO_LARGE (-8)         /* per-trajectory working set exceeds LDS */
+
+/* Per-trajectory status bits (status[b]). */
+#define MTG_TRAJ_OK 0
+#define MTG_TRAJ_BAD_TIME 1            /* some T <= 0, < DBL_EPSILON or not finite (CHECK_GT lin_impl:287) */
+#define MTG_TRAJ_NOT_SPD 2             /* non-positive pivot in R_pp (reference: undetected, lin_impl:355-368) */
+#define MTG_TRAJ_WARN_DROPPED 256      /* constraint of order > N/2-1 ignored (LOG(WARNING) lin_impl:84-87) */
+#define MTG_TRAJ_ERROR_MASK 255
+
+/* Flags. */
+#define MTG_FLAG_DEVICE_PTRS 1u        /* all array arguments are device pointers on the ctx device */
+#define MTG_FLAG_ASYNC 2u              /* do not synchronize the stream before returning */
+#define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
+
+typedef struct mtg_ctx mtg_ctx;
+
+/* Version / diagnostics. */
+int mtg_abi_version(void);
+const char* mtg_status_string(int code);
+const char* mtg_last_error(mtg_ctx* ctx);
+
+/* Devices and contexts.  A context owns a HIP stream on one device plus
+ * staging buffers for host-pointer calls. */
+int mtg_device_count(int* count);
+int mtg_create(int device, mtg_ctx** out_ctx);
+int mtg_destroy(mtg_ctx* ctx);
+/* Launch on an external hipStream_t (e.g. torch's current stream); NULL
+ * restores the context's own stream. */
+int mtg_set_stream(mtg_ctx* ctx, void* hip_stream);
+void* mtg_get_stream(mtg_ctx* ctx);
+int mtg_synchronize(mtg_ctx* ctx);
+
+/* Batched setupFromVertices + solveLinear.  Replaces, per trajectory,
+ *   PolynomialOptimization<N>(D)                 lin_impl:33-44
+ *   setupFromVertices(vertices, times, r)        lin_impl:47-99
+ *     updateSegmentTimes                         lin_impl:276-295
+ *     setupConstraintReorderingMatrix            lin_impl:172-250
+ *   solveLinear()                                lin_impl:329-369
+ *     constructR + SparseQR + per-dim solve      lin_impl:298-365
+ *     updateSegmentsFromCompactConstraints       lin_impl:253-273
+ *   getSegments / getFreeConstraints / computeCost.
+ * One call solves B independent problems of identical shape (N, D, K, r);
+ * masks and values may differ per trajectory. */
+int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                           int64_t batch, const double* values, const uint8_t* fixed_mask,
+                           const double* times, double* coeffs, double* free_out,
+                           int32_t* n_free_out, double* cost_out, int32_t* status,
+                           unsigned flags);
+
+/* Batched Trajectory::evaluateRange (src/trajectory.cpp:68-128) over solved
+ * trajectories, with the reference's sequential time accumulation (acc += dt)
+ * reproduced exactly.  coeffs [B][K][D][N], times [B][K].  Sample counts are
+ * ragged: first call with out == NULL to get counts[B] (samples per
+ * trajectory); then pass offsets[B] (exclusive prefix sum of counts, in
+ * samples) and out [sum(counts)][D] (+ optional sample_times [sum]).
+ * t_start/t_end/dt are shared by the whole batch; derivative selects the
+ * derivative order evaluated (Polynomial::evaluate, polynomial.h:138-151). */
+int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
+                             const double* coeffs, const double* times, double t_start,
+                             double t_end, double dt, int derivative, int64_t* counts,
+                             const int64_t* offsets, double* out, double* sample_times,
+                             unsigned flags);
+
+/* Batched segment-time sweep (the nonlinear time-allocation objective,
+ * polynomial_optimization_nonlinear_impl.h:765-832 via updateSegmentTimes +
+ * solveLinear + computeCost): for each trajectory b and candidate c the
+ * times are scale[c] * times[b][:] and the result is the optimal cost
+ * J(b, c) (computeCost()).  cost_out [B][C]. */
+int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                         int64_t batch, const double* values, const uint8_t* fixed_mask,
+                         const double* times, int n_candidates, const double* scales,
+                         double* cost_out, int32_t* status, unsigned flags);
+
+/* Timing of the most recent kernel launch(es) of this context on its stream
+ * (hipEvent pair around the solve kernel), in milliseconds. */
+int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);
+
+/* ---- Host utilities (no GPU): the reference's synthetic-input generators,
+ * bit-exact with libstdc++ <random>, packed straight into the ABI layout.
+ * Trajectory b of a batch uses seed (seed0 + b).  values [B][V][h][D],
+ * fixed_mask [B][V]; derivatives above N/2-1 set the WARN_DROPPED bit in the
+ * returned mask (bit 7) and are otherwise ignored, as setupFromVertices does. */
+/* createRandomVertices (src/vertex.cpp:27-79) + estimateSegmentTimes (:162-178) */
+int mtg_host_random_vertices_batch(int N, int D, int K, int max_derivative, const double* pos_min,
+                                   const double* pos_max, uint32_t seed0, int64_t batch,
+                                   double v_max, double a_max, double magic_fabian_constant,
+                                   double* values, uint8_t* fixed_mask, double* times,
+                                   int threads);
+/* createRandomVerticesPath (src/polynomial_timing_evaluation.cpp:34-91) +
+ * estimateSegmentTimes(v_max, a_max, magic) as timeEval does (:93-112) */
+int mtg_host_random_vertices_path_batch(int N, int D, int K, double average_distance,
+                                        int max_derivative, uint32_t seed0, int64_t batch,
+                                        double v_max, double a_max, double magic_fabian_constant,
+                                        double* values, uint8_t* fixed_mask, double* times,
+                                        int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTG_H_ */

@@ -1,0 +1,115 @@
+"""ctypes binding of libmtg.so (include/mtg.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU
+is visible, calls raise.  PyTorch is only used (in solver.py) as an optional
+holder of device memory and streams.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libmtg.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "mtg.h")
+
+MTG_OK = 0
+MTG_ERR_INVALID_ARGUMENT = -1
+MTG_ERR_UNSUPPORTED_N = -2
+MTG_ERR_BAD_DERIVATIVE = -3
+MTG_ERR_SIZE_MISMATCH = -4
+MTG_ERR_HIP = -5
+MTG_ERR_NO_DEVICE = -6
+MTG_ERR_OUT_OF_MEMORY = -7
+MTG_ERR_TOO_LARGE = -8
+
+MTG_TRAJ_OK = 0
+MTG_TRAJ_BAD_TIME = 1
+MTG_TRAJ_NOT_SPD = 2
+MTG_TRAJ_WARN_DROPPED = 256
+MTG_TRAJ_ERROR_MASK = 255
+
+MTG_FLAG_DEVICE_PTRS = 1
+MTG_FLAG_ASYNC = 2
+MTG_FLAG_SPLIT_KERNELS = 4
+
+_c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
+
+_SIGNATURES = {
+    "mtg_abi_version": (ctypes.c_int, []),
+    "mtg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "mtg_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "mtg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "mtg_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "mtg_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "mtg_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mtg_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
+    "mtg_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "mtg_solve_linear_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp,
+                                              _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_evaluate_range_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int64, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double,
+                                                ctypes.c_double, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
+                                                ctypes.c_uint]),
+    "mtg_time_sweep_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_int,
+                                            _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_last_kernel_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "mtg_host_random_vertices_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                      _c_dp, _c_dp, ctypes.c_uint32, ctypes.c_int64,
+                                                      ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                                      _c_dp, _c_dp, _c_dp, ctypes.c_int]),
+    "mtg_host_random_vertices_path_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                           ctypes.c_double, ctypes.c_int, ctypes.c_uint32,
+                                                           ctypes.c_int64, ctypes.c_double, ctypes.c_double,
+                                                           ctypes.c_double, _c_dp, _c_dp, _c_dp,
+                                                           ctypes.c_int]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class MTGError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("%s (code %d)" % (message, code))
+        self.code = code
+
+
+def load(path=None):
+    """Load libmtg.so; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("MTG_LIBRARY", LIB_PATH)
+    if not os.path.exists(p):
+        raise MTGError(MTG_ERR_NO_DEVICE, "libmtg.so not found at %s: run __graft_entry__.build()" % p)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def status_string(code):
+    return load().mtg_status_string(code).decode()
+
+
+def check(code, ctx=None):
+    if code != MTG_OK:
+        msg = status_string(code)
+        if ctx is not None:
+            detail = load().mtg_last_error(ctx)
+            if detail:
+                msg += ": " + detail.decode()
+        raise MTGError(code, msg)
+    return code
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    rc = load().mtg_device_count(ctypes.byref(n))
+    return n.value if rc == MTG_OK else 0

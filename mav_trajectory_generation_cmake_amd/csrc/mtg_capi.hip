@@ -1,0 +1,371 @@
+// mtg_capi.hip -- the C ABI (include/mtg.h): contexts, staging, launches.
+// Never aborts, never throws across the boundary; errors are return codes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "mtg.h"
+#include "mtg_internal.h"
+
+struct mtg_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  void* staging = nullptr;
+  size_t staging_bytes = 0;
+  void* workspace = nullptr;
+  size_t workspace_bytes = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  std::string last_error;
+  std::mutex mu;
+};
+
+namespace {
+
+int set_hip_error(mtg_ctx* ctx, hipError_t e, const char* what) {
+  if (ctx) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    ctx->last_error = buf;
+  }
+  return e == hipErrorOutOfMemory ? MTG_ERR_OUT_OF_MEMORY : MTG_ERR_HIP;
+}
+
+int set_error(mtg_ctx* ctx, int code, const char* what) {
+  if (ctx) ctx->last_error = what;
+  return code;
+}
+
+#define MTG_HIP_TRY(ctx, expr)                          \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) return set_hip_error(ctx, e_, #expr); \
+  } while (0)
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+hipError_t ensure(void** buf, size_t* have, size_t need) {
+  if (*have >= need) return hipSuccess;
+  if (*buf) {
+    hipError_t e = hipFree(*buf);
+    if (e != hipSuccess) return e;
+    *buf = nullptr;
+    *have = 0;
+  }
+  hipError_t e = hipMalloc(buf, need);
+  if (e == hipSuccess) *have = need;
+  return e;
+}
+
+int check_shape(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  if (N < 2 || N > 12 || (N % 2)) return set_error(ctx, MTG_ERR_UNSUPPORTED_N, "N must be even and in [2, 12]");
+  if (r < 0 || r > N / 2 - 1)
+    return set_error(ctx, MTG_ERR_BAD_DERIVATIVE, "derivative_to_optimize must be in [0, N/2-1]");
+  if (K < 1 || D < 1 || batch < 0) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "need K >= 1, D >= 1, batch >= 0");
+  int lg, tpb;
+  size_t lds;
+  if (!mtg::solve_geometry(N, D, K, &lg, &lds, &tpb))
+    return set_error(ctx, MTG_ERR_TOO_LARGE, "per-trajectory working set exceeds LDS (reduce K or D)");
+  return MTG_OK;
+}
+
+// Shared body of solve / time-sweep: stage host buffers if needed, launch, copy back.
+int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const double* values,
+              const uint8_t* mask, const double* times, double* coeffs, double* free_out,
+              int32_t* n_free_out, double* cost_out, int32_t* status, int n_cand,
+              const double* scales, unsigned flags) {
+  const int V = K + 1, h = N / 2;
+  const int64_t pairs = batch * n_cand;
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  mtg::SolveArgs a{};
+  a.B = pairs;
+  a.K = K;
+  a.D = D;
+  a.r = r;
+  a.n_cand = n_cand;
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  const size_t b_vals = sizeof(double) * (size_t)batch * V * h * D;
+  const size_t b_mask = sizeof(uint8_t) * (size_t)batch * V;
+  const size_t b_times = sizeof(double) * (size_t)batch * K;
+  const size_t b_scales = scales ? sizeof(double) * (size_t)n_cand : 0;
+  const size_t b_coeffs = coeffs ? sizeof(double) * (size_t)pairs * K * D * N : 0;
+  const size_t b_free = free_out ? sizeof(double) * (size_t)pairs * D * V * h : 0;
+  const size_t b_nfree = n_free_out ? sizeof(int32_t) * (size_t)pairs : 0;
+  const size_t b_cost = cost_out ? sizeof(double) * (size_t)pairs : 0;
+  const size_t b_status = status ? sizeof(int32_t) * (size_t)pairs : 0;
+  char* base = nullptr;
+  size_t o_vals = 0, o_mask = 0, o_times = 0, o_scales = 0, o_coeffs = 0, o_free = 0, o_nfree = 0,
+         o_cost = 0, o_status = 0;
+  if (dev) {
+    a.values = values;
+    a.mask = mask;
+    a.times = times;
+    a.scales = scales;
+    a.coeffs = coeffs;
+    a.free_out = free_out;
+    a.n_free_out = n_free_out;
+    a.cost_out = cost_out;
+    a.status = status;
+  } else {
+    size_t off = 0;
+    o_vals = off; off = align_up(off + b_vals);
+    o_mask = off; off = align_up(off + b_mask);
+    o_times = off; off = align_up(off + b_times);
+    o_scales = off; off = align_up(off + b_scales);
+    o_coeffs = off; off = align_up(off + b_coeffs);
+    o_free = off; off = align_up(off + b_free);
+    o_nfree = off; off = align_up(off + b_nfree);
+    o_cost = off; off = align_up(off + b_cost);
+    o_status = off; off = align_up(off + b_status);
+    MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+    base = static_cast<char*>(ctx->staging);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_vals, values, b_vals, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_mask, mask, b_mask, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+    if (scales)
+      MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_scales, scales, b_scales, hipMemcpyHostToDevice, ctx->stream));
+    a.values = reinterpret_cast<const double*>(base + o_vals);
+    a.mask = reinterpret_cast<const uint8_t*>(base + o_mask);
+    a.times = reinterpret_cast<const double*>(base + o_times);
+    a.scales = scales ? reinterpret_cast<const double*>(base + o_scales) : nullptr;
+    a.coeffs = coeffs ? reinterpret_cast<double*>(base + o_coeffs) : nullptr;
+    a.free_out = free_out ? reinterpret_cast<double*>(base + o_free) : nullptr;
+    a.n_free_out = n_free_out ? reinterpret_cast<int32_t*>(base + o_nfree) : nullptr;
+    a.cost_out = cost_out ? reinterpret_cast<double*>(base + o_cost) : nullptr;
+    a.status = status ? reinterpret_cast<int32_t*>(base + o_status) : nullptr;
+  }
+  if (free_out && b_free) {
+    // entries beyond n_free are left zero
+    MTG_HIP_TRY(ctx, hipMemsetAsync(const_cast<double*>(a.free_out), 0, b_free, ctx->stream));
+  }
+  MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  if (flags & MTG_FLAG_SPLIT_KERNELS) {
+    const size_t ws = mtg::split_workspace_bytes(N, D, K, pairs);
+    MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
+    MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
+  } else {
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream));
+  }
+  MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  ctx->timed = true;
+  if (!dev) {
+    if (coeffs) MTG_HIP_TRY(ctx, hipMemcpyAsync(coeffs, base + o_coeffs, b_coeffs, hipMemcpyDeviceToHost, ctx->stream));
+    if (free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(free_out, base + o_free, b_free, hipMemcpyDeviceToHost, ctx->stream));
+    if (n_free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(n_free_out, base + o_nfree, b_nfree, hipMemcpyDeviceToHost, ctx->stream));
+    if (cost_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(cost_out, base + o_cost, b_cost, hipMemcpyDeviceToHost, ctx->stream));
+    if (status) MTG_HIP_TRY(ctx, hipMemcpyAsync(status, base + o_status, b_status, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  } else if (!(flags & MTG_FLAG_ASYNC)) {
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return MTG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtg_abi_version(void) { return MTG_ABI_VERSION; }
+
+const char* mtg_status_string(int code) {
+  switch (code) {
+    case MTG_OK: return "ok";
+    case MTG_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case MTG_ERR_UNSUPPORTED_N: return "unsupported N (even, 2..12)";
+    case MTG_ERR_BAD_DERIVATIVE: return "derivative_to_optimize out of [0, N/2-1]";
+    case MTG_ERR_SIZE_MISMATCH: return "size mismatch";
+    case MTG_ERR_HIP: return "HIP runtime error";
+    case MTG_ERR_NO_DEVICE: return "no HIP device";
+    case MTG_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case MTG_ERR_TOO_LARGE: return "problem too large for the LDS-resident solver";
+    default: return "unknown status";
+  }
+}
+
+const char* mtg_last_error(mtg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int mtg_device_count(int* count) {
+  if (!count) return MTG_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return e == hipErrorNoDevice ? MTG_ERR_NO_DEVICE : MTG_ERR_HIP;
+  }
+  *count = n;
+  return MTG_OK;
+}
+
+int mtg_create(int device, mtg_ctx** out_ctx) {
+  if (!out_ctx) return MTG_ERR_INVALID_ARGUMENT;
+  *out_ctx = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return MTG_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return MTG_ERR_INVALID_ARGUMENT;
+  mtg_ctx* ctx = new (std::nothrow) mtg_ctx();
+  if (!ctx) return MTG_ERR_OUT_OF_MEMORY;
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+  if (e != hipSuccess) {
+    mtg_destroy(ctx);
+    return MTG_ERR_HIP;
+  }
+  ctx->stream = ctx->own_stream;
+  *out_ctx = ctx;
+  return MTG_OK;
+}
+
+int mtg_destroy(mtg_ctx* ctx) {
+  if (!ctx) return MTG_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->staging) (void)hipFree(ctx->staging);
+  if (ctx->workspace) (void)hipFree(ctx->workspace);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+  return MTG_OK;
+}
+
+int mtg_set_stream(mtg_ctx* ctx, void* hip_stream) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  return MTG_OK;
+}
+
+void* mtg_get_stream(mtg_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int mtg_synchronize(mtg_ctx* ctx) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MTG_OK;
+}
+
+int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                           int64_t batch, const double* values, const uint8_t* fixed_mask,
+                           const double* times, double* coeffs, double* free_out,
+                           int32_t* n_free_out, double* cost_out, int32_t* status,
+                           unsigned flags) {
+  int rc = check_shape(ctx, N, D, K, derivative_to_optimize, batch);
+  if (rc != MTG_OK) return rc;
+  if (batch == 0) return MTG_OK;
+  if (!values || !fixed_mask || !times)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "values, fixed_mask and times are required");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return run_solve(ctx, N, D, K, derivative_to_optimize, batch, values, fixed_mask, times, coeffs,
+                   free_out, n_free_out, cost_out, status, 1, nullptr, flags);
+}
+
+int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                         int64_t batch, const double* values, const uint8_t* fixed_mask,
+                         const double* times, int n_candidates, const double* scales,
+                         double* cost_out, int32_t* status, unsigned flags) {
+  int rc = check_shape(ctx, N, D, K, derivative_to_optimize, batch);
+  if (rc != MTG_OK) return rc;
+  if (n_candidates < 1) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "n_candidates must be >= 1");
+  if (batch == 0) return MTG_OK;
+  if (!values || !fixed_mask || !times || !scales || !cost_out)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "values, fixed_mask, times, scales, cost_out are required");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return run_solve(ctx, N, D, K, derivative_to_optimize, batch, values, fixed_mask, times, nullptr,
+                   nullptr, nullptr, cost_out, status, n_candidates, scales,
+                   flags & ~MTG_FLAG_SPLIT_KERNELS);
+}
+
+int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
+                             const double* coeffs, const double* times, double t_start,
+                             double t_end, double dt, int derivative, int64_t* counts,
+                             const int64_t* offsets, double* out, double* sample_times,
+                             unsigned flags) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  if (N < 2 || N > 12 || (N % 2)) return set_error(ctx, MTG_ERR_UNSUPPORTED_N, "N must be even and in [2, 12]");
+  if (K < 1 || D < 1 || batch < 0) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "need K >= 1, D >= 1, batch >= 0");
+  if (!(dt > 0.0) || derivative < 0)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "dt must be > 0 and derivative >= 0");
+  if (batch == 0) return MTG_OK;
+  if (!times || !counts || (out && (!coeffs || !offsets)))
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "times and counts required; out needs coeffs and offsets");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  if (dev) {
+    if (!out) {
+      MTG_HIP_TRY(ctx, mtg::launch_eval_count(N, D, K, batch, times, t_start, t_end, dt, counts, ctx->stream));
+    } else {
+      MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+      MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative,
+                                              offsets, out, sample_times, ctx->stream));
+      MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+      ctx->timed = true;
+    }
+    if (!(flags & MTG_FLAG_ASYNC)) MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return MTG_OK;
+  }
+  // Host pointers: stage everything.
+  const size_t b_times = sizeof(double) * (size_t)batch * K;
+  const size_t b_coeffs = coeffs ? sizeof(double) * (size_t)batch * K * D * N : 0;
+  const size_t b_counts = sizeof(int64_t) * (size_t)batch;
+  int64_t total = 0;
+  if (out) {
+    for (int64_t b = 0; b < batch; ++b) total = std::max<int64_t>(total, offsets[b] + counts[b]);
+  }
+  const size_t b_out = out ? sizeof(double) * (size_t)total * D : 0;
+  const size_t b_st = (out && sample_times) ? sizeof(double) * (size_t)total : 0;
+  size_t off = 0;
+  const size_t o_times = off; off = align_up(off + b_times);
+  const size_t o_coeffs = off; off = align_up(off + b_coeffs);
+  const size_t o_counts = off; off = align_up(off + b_counts);
+  const size_t o_offsets = off; off = align_up(off + b_counts);
+  const size_t o_out = off; off = align_up(off + b_out);
+  const size_t o_st = off; off = align_up(off + b_st);
+  MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+  char* base = static_cast<char*>(ctx->staging);
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+  if (!out) {
+    MTG_HIP_TRY(ctx, mtg::launch_eval_count(N, D, K, batch, reinterpret_cast<double*>(base + o_times), t_start,
+                                            t_end, dt, reinterpret_cast<int64_t*>(base + o_counts), ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(counts, base + o_counts, b_counts, hipMemcpyDeviceToHost, ctx->stream));
+  } else {
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coeffs, coeffs, b_coeffs, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_offsets, offsets, b_counts, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<double*>(base + o_coeffs),
+                                            reinterpret_cast<double*>(base + o_times), t_start, t_end, dt,
+                                            derivative, reinterpret_cast<int64_t*>(base + o_offsets),
+                                            reinterpret_cast<double*>(base + o_out),
+                                            sample_times ? reinterpret_cast<double*>(base + o_st) : nullptr,
+                                            ctx->stream));
+    MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    ctx->timed = true;
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(out, base + o_out, b_out, hipMemcpyDeviceToHost, ctx->stream));
+    if (sample_times) MTG_HIP_TRY(ctx, hipMemcpyAsync(sample_times, base + o_st, b_st, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MTG_OK;
+}
+
+int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms) {
+  if (!ctx || !ms) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->timed) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "no timed launch yet");
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  MTG_HIP_TRY(ctx, hipEventSynchronize(ctx->ev1));
+  MTG_HIP_TRY(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+  return MTG_OK;
+}
+
+}  // extern "C"

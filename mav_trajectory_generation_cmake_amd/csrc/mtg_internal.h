@@ -1,0 +1,46 @@
+// Internal declarations shared by the kernels (mtg_kernels.hip) and the C ABI
+// (mtg_capi.hip).  Not installed; the public surface is include/mtg.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mtg {
+
+// Arguments of one batched solve launch.  Pointers are device pointers.
+struct SolveArgs {
+  const double* values;   // [B][V][h][D]
+  const uint8_t* mask;    // [B][V]
+  const double* times;    // [B][K]
+  double* coeffs;         // [B][K][D][N]
+  double* free_out;       // [B][D][V*h]  (nullable)
+  int32_t* n_free_out;    // [B]          (nullable)
+  double* cost_out;       // [B]          (nullable)
+  int32_t* status;        // [B]          (nullable)
+  const double* scales;   // time-sweep candidate scales [C] (nullable: plain solve)
+  int64_t B;              // trajectories (or trajectory x candidate pairs for the sweep)
+  int K, D, r;
+  int n_cand;             // candidates per trajectory for the sweep (1 for a plain solve)
+};
+
+// Lanes per trajectory and LDS bytes per workgroup for a shape; returns false
+// when the per-trajectory working set cannot fit in LDS.
+bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes, int* traj_per_block);
+
+// Launch the fused solve kernel on `stream`.
+hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream);
+
+// Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
+// workspace, then the block-Cholesky solve + recovery.
+size_t split_workspace_bytes(int N, int D, int K, int64_t B);
+hipError_t launch_solve_split(int N, const SolveArgs& a, void* workspace, hipStream_t stream);
+
+// evaluateRange
+hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
+                             double t_end, double dt, int64_t* counts, hipStream_t stream);
+hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs,
+                             const double* times, double t_start, double t_end, double dt,
+                             int derivative, const int64_t* offsets, double* out,
+                             double* sample_times, hipStream_t stream);
+
+}  // namespace mtg

@@ -1,0 +1,207 @@
+"""Batched solver API over the C ABI (libmtg.so).
+
+Arrays may be numpy arrays (host; the library stages them through HBM) or
+torch CUDA tensors (device-resident; launched on torch's current stream so
+torch.cuda.Event timing and stream ordering work).  There is no CPU path.
+
+Layouts follow include/mtg.h:
+  values [B][K+1][N/2][D] float64, mask [B][K+1] uint8, times [B][K] float64
+  coeffs [B][K][D][N], free [B][D][(K+1)*N/2], n_free [B], cost [B], status [B]
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _addr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+class Context:
+    """Owns one mtg_ctx (a HIP stream + staging buffers on one device)."""
+
+    def __init__(self, device=0):
+        self._lib = nat.load()
+        h = ctypes.c_void_p()
+        nat.check(self._lib.mtg_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self._lib.mtg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_handle):
+        """stream_handle: an int hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or None."""
+        nat.check(self._lib.mtg_set_stream(self.handle, stream_handle), self.handle)
+
+    def synchronize(self):
+        nat.check(self._lib.mtg_synchronize(self.handle), self.handle)
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float(0)
+        nat.check(self._lib.mtg_last_kernel_ms(self.handle, ctypes.byref(ms)), self.handle)
+        return ms.value
+
+    # ------------------------------------------------------------------ solve
+    def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
+                           cost=None, status=None, split=False, asynchronous=False):
+        """Solve a batch; returns dict of outputs (allocates those not given).
+
+        want-flags: pass arrays (or True to allocate) for free / n_free / cost / status."""
+        dev = _is_torch(values) and values.is_cuda
+        B, V, h, D = values.shape
+        K = V - 1
+        assert h == N // 2, "values must be [B][K+1][N/2][D]"
+        assert tuple(mask.shape) == (B, V) and tuple(times.shape) == (B, K)
+        out = {}
+
+        def alloc(name, arr, shape, dtype):
+            if arr is None or arr is False:
+                return None
+            if arr is True:
+                if dev:
+                    import torch
+                    tdt = {np.float64: torch.float64, np.int32: torch.int32}[dtype]
+                    arr = torch.empty(shape, dtype=tdt, device=values.device)
+                else:
+                    arr = np.empty(shape, dtype=dtype)
+            out[name] = arr
+            return arr
+
+        coeffs = alloc("coeffs", True if coeffs is None else coeffs, (B, K, D, N), np.float64)
+        free = alloc("free", free, (B, D, V * h), np.float64)
+        n_free = alloc("n_free", n_free, (B,), np.int32)
+        cost = alloc("cost", cost, (B,), np.float64)
+        status = alloc("status", status, (B,), np.int32)
+        flags = 0
+        if dev:
+            import torch
+            flags |= nat.MTG_FLAG_DEVICE_PTRS
+            self.set_stream(torch.cuda.current_stream(values.device).cuda_stream)
+            if asynchronous:
+                flags |= nat.MTG_FLAG_ASYNC
+        else:
+            values = np.ascontiguousarray(values, dtype=np.float64)
+            mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            times = np.ascontiguousarray(times, dtype=np.float64)
+        if split:
+            flags |= nat.MTG_FLAG_SPLIT_KERNELS
+        rc = self._lib.mtg_solve_linear_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
+                                              _addr(times), _addr(coeffs), _addr(free), _addr(n_free),
+                                              _addr(cost), _addr(status), flags)
+        nat.check(rc, self.handle)
+        return out
+
+    def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
+                         asynchronous=False):
+        dev = _is_torch(values) and values.is_cuda
+        B, V, h, D = values.shape
+        K = V - 1
+        C = len(scales)
+        if dev:
+            import torch
+            cost = cost if cost is not None else torch.empty((B, C), dtype=torch.float64, device=values.device)
+            flags = nat.MTG_FLAG_DEVICE_PTRS | (nat.MTG_FLAG_ASYNC if asynchronous else 0)
+            self.set_stream(torch.cuda.current_stream(values.device).cuda_stream)
+        else:
+            values = np.ascontiguousarray(values, dtype=np.float64)
+            mask = np.ascontiguousarray(mask, dtype=np.uint8)
+            times = np.ascontiguousarray(times, dtype=np.float64)
+            scales = np.ascontiguousarray(scales, dtype=np.float64)
+            cost = cost if cost is not None else np.empty((B, C))
+            flags = 0
+        rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
+                                            _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
+        nat.check(rc, self.handle)
+        return cost
+
+    # ------------------------------------------------------- evaluateRange
+    def evaluate_range_batch(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True):
+        """Host-array convenience wrapper: returns (samples [S][D], sample_times [S], counts [B], offsets [B])."""
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        B, K, D, N = coeffs.shape
+        counts = np.zeros(B, dtype=np.int64)
+        nat.check(self._lib.mtg_evaluate_range_batch(self.handle, N, D, K, B, None, _addr(times), t_start, t_end,
+                                                     dt, derivative, _addr(counts), None, None, None, 0),
+                  self.handle)
+        offsets = np.zeros(B, dtype=np.int64)
+        if B > 1:
+            offsets[1:] = np.cumsum(counts)[:-1]
+        total = int(counts.sum())
+        out = np.zeros((max(total, 1), D))
+        st = np.zeros(max(total, 1)) if want_times else None
+        nat.check(self._lib.mtg_evaluate_range_batch(self.handle, N, D, K, B, _addr(coeffs), _addr(times), t_start,
+                                                     t_end, dt, derivative, _addr(counts), _addr(offsets),
+                                                     _addr(out), _addr(st), 0), self.handle)
+        return out[:total], (st[:total] if want_times else None), counts, offsets
+
+
+_default_ctx = {}
+
+
+def default_context(device=0):
+    ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = _default_ctx[device] = Context(device)
+    return ctx
+
+
+def solve_linear_batch(N, r, values, mask, times, device=0, **kw):
+    return default_context(device).solve_linear_batch(N, r, values, mask, times, **kw)
+
+
+# ----------------------------------------------------------------- generators
+def random_vertices_path_batch(N, D, K, batch, seed0=0, average_distance=5.0, max_derivative=4,
+                               v_max=2.0, a_max=2.0, magic=6.5, threads=0):
+    """The reference bench generator (src/polynomial_timing_evaluation.cpp:34-112), seeds seed0..seed0+B-1."""
+    lib = nat.load()
+    V, h = K + 1, N // 2
+    values = np.zeros((batch, V, h, D))
+    mask = np.zeros((batch, V), dtype=np.uint8)
+    times = np.zeros((batch, K))
+    nat.check(lib.mtg_host_random_vertices_path_batch(N, D, K, average_distance, max_derivative, seed0, batch,
+                                                      v_max, a_max, magic, _addr(values), _addr(mask),
+                                                      _addr(times), threads))
+    return values, mask, times
+
+
+def random_vertices_batch(N, D, K, batch, pos_min, pos_max, seed0=0, max_derivative=4, v_max=3.0, a_max=5.0,
+                          magic=6.5, threads=0):
+    """createRandomVertices + estimateSegmentTimes (src/vertex.cpp:27-79, :162-178)."""
+    lib = nat.load()
+    V, h = K + 1, N // 2
+    pos_min = np.ascontiguousarray(pos_min, dtype=np.float64)
+    pos_max = np.ascontiguousarray(pos_max, dtype=np.float64)
+    assert len(pos_min) == D and len(pos_max) == D
+    values = np.zeros((batch, V, h, D))
+    mask = np.zeros((batch, V), dtype=np.uint8)
+    times = np.zeros((batch, K))
+    nat.check(lib.mtg_host_random_vertices_batch(N, D, K, max_derivative, _addr(pos_min), _addr(pos_max), seed0,
+                                                 batch, v_max, a_max, magic, _addr(values), _addr(mask),
+                                                 _addr(times), threads))
+    return values, mask, times
