@@ -82,9 +82,11 @@ const char* mtg_last_error(mtg_ctx* ctx);
 int mtg_device_count(int* count);
 int mtg_create(int device, mtg_ctx** out_ctx);
 int mtg_destroy(mtg_ctx* ctx);
-/* Launch on an external hipStream_t (e.g. torch's current stream); NULL
- * restores the context's own stream. */
+/* Launch on an external hipStream_t (e.g. torch's current stream).  NULL
+ * selects the HIP null (default) stream; mtg_reset_stream restores the
+ * context's own stream. */
 int mtg_set_stream(mtg_ctx* ctx, void* hip_stream);
+int mtg_reset_stream(mtg_ctx* ctx);
 void* mtg_get_stream(mtg_ctx* ctx);
 int mtg_synchronize(mtg_ctx* ctx);
 
@@ -132,6 +134,12 @@ int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_op
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);
+/* Keep a HIP event pair per launch for the last `ring` launches (ring >= 1;
+ * the default is 1).  mtg_kernel_times synchronizes on the newest event and
+ * writes up to n durations (ms, oldest first) of the launches still in the
+ * ring; *n_out receives the count. */
+int mtg_enable_timing(mtg_ctx* ctx, int ring);
+int mtg_kernel_times(mtg_ctx* ctx, float* ms, int n, int* n_out);
 
 /* ---- Host utilities (no GPU): the reference's synthetic-input generators,
  * bit-exact with libstdc++ <random>, packed straight into the ABI layout.

@@ -41,6 +41,7 @@ _SIGNATURES = {
     "mtg_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "mtg_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "mtg_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mtg_reset_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "mtg_get_stream": (ctypes.c_void_p, [ctypes.c_void_p]),
     "mtg_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "mtg_solve_linear_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -54,6 +55,9 @@ _SIGNATURES = {
                                             ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_int,
                                             _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
     "mtg_last_kernel_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "mtg_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mtg_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int)]),
     "mtg_host_random_vertices_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                       _c_dp, _c_dp, ctypes.c_uint32, ctypes.c_int64,
                                                       ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -8,6 +8,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "mtg.h"
 #include "mtg_internal.h"
@@ -20,8 +21,9 @@ struct mtg_ctx {
   size_t staging_bytes = 0;
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
+  // ring of (start, stop) events around kernel launches; launches counts recorded launches
+  std::vector<hipEvent_t> ev_start, ev_stop;
+  int64_t launches = 0;
   std::string last_error;
   std::mutex mu;
 };
@@ -61,6 +63,42 @@ hipError_t ensure(void** buf, size_t* have, size_t need) {
   hipError_t e = hipMalloc(buf, need);
   if (e == hipSuccess) *have = need;
   return e;
+}
+
+hipError_t time_begin(mtg_ctx* ctx) {
+  const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
+  return hipEventRecord(ctx->ev_start[slot], ctx->stream);
+}
+
+hipError_t time_end(mtg_ctx* ctx) {
+  const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
+  hipError_t e = hipEventRecord(ctx->ev_stop[slot], ctx->stream);
+  if (e == hipSuccess) ctx->launches++;
+  return e;
+}
+
+void destroy_events(mtg_ctx* ctx) {
+  for (hipEvent_t e : ctx->ev_start) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->ev_stop) (void)hipEventDestroy(e);
+  ctx->ev_start.clear();
+  ctx->ev_stop.clear();
+  ctx->launches = 0;
+}
+
+hipError_t create_events(mtg_ctx* ctx, int ring) {
+  destroy_events(ctx);
+  for (int i = 0; i < ring; ++i) {
+    hipEvent_t a = nullptr, b = nullptr;
+    hipError_t e = hipEventCreate(&a);
+    if (e == hipSuccess) e = hipEventCreate(&b);
+    if (e != hipSuccess) {
+      if (a) (void)hipEventDestroy(a);
+      return e;
+    }
+    ctx->ev_start.push_back(a);
+    ctx->ev_stop.push_back(b);
+  }
+  return hipSuccess;
 }
 
 int check_shape(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch) {
@@ -145,7 +183,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     // entries beyond n_free are left zero
     MTG_HIP_TRY(ctx, hipMemsetAsync(const_cast<double*>(a.free_out), 0, b_free, ctx->stream));
   }
-  MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  MTG_HIP_TRY(ctx, time_begin(ctx));
   if (flags & MTG_FLAG_SPLIT_KERNELS) {
     const size_t ws = mtg::split_workspace_bytes(N, D, K, pairs);
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
@@ -153,8 +191,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   } else {
     MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream));
   }
-  MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-  ctx->timed = true;
+  MTG_HIP_TRY(ctx, time_end(ctx));
   if (!dev) {
     if (coeffs) MTG_HIP_TRY(ctx, hipMemcpyAsync(coeffs, base + o_coeffs, b_coeffs, hipMemcpyDeviceToHost, ctx->stream));
     if (free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(free_out, base + o_free, b_free, hipMemcpyDeviceToHost, ctx->stream));
@@ -214,8 +251,7 @@ int mtg_create(int device, mtg_ctx** out_ctx) {
   ctx->device = device;
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+  if (e == hipSuccess) e = create_events(ctx, 1);
   if (e != hipSuccess) {
     mtg_destroy(ctx);
     return MTG_ERR_HIP;
@@ -231,8 +267,7 @@ int mtg_destroy(mtg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->staging) (void)hipFree(ctx->staging);
   if (ctx->workspace) (void)hipFree(ctx->workspace);
-  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  destroy_events(ctx);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
   return MTG_OK;
@@ -241,7 +276,14 @@ int mtg_destroy(mtg_ctx* ctx) {
 int mtg_set_stream(mtg_ctx* ctx, void* hip_stream) {
   if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> g(ctx->mu);
-  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  ctx->stream = static_cast<hipStream_t>(hip_stream);  // NULL = the HIP null stream
+  return MTG_OK;
+}
+
+int mtg_reset_stream(mtg_ctx* ctx) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->stream = ctx->own_stream;
   return MTG_OK;
 }
 
@@ -306,11 +348,10 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
     if (!out) {
       MTG_HIP_TRY(ctx, mtg::launch_eval_count(N, D, K, batch, times, t_start, t_end, dt, counts, ctx->stream));
     } else {
-      MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+      MTG_HIP_TRY(ctx, time_begin(ctx));
       MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative,
                                               offsets, out, sample_times, ctx->stream));
-      MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-      ctx->timed = true;
+      MTG_HIP_TRY(ctx, time_end(ctx));
     }
     if (!(flags & MTG_FLAG_ASYNC)) MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return MTG_OK;
@@ -342,15 +383,14 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
   } else {
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coeffs, coeffs, b_coeffs, hipMemcpyHostToDevice, ctx->stream));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_offsets, offsets, b_counts, hipMemcpyHostToDevice, ctx->stream));
-    MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    MTG_HIP_TRY(ctx, time_begin(ctx));
     MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<double*>(base + o_coeffs),
                                             reinterpret_cast<double*>(base + o_times), t_start, t_end, dt,
                                             derivative, reinterpret_cast<int64_t*>(base + o_offsets),
                                             reinterpret_cast<double*>(base + o_out),
                                             sample_times ? reinterpret_cast<double*>(base + o_st) : nullptr,
                                             ctx->stream));
-    MTG_HIP_TRY(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    ctx->timed = true;
+    MTG_HIP_TRY(ctx, time_end(ctx));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(out, base + o_out, b_out, hipMemcpyDeviceToHost, ctx->stream));
     if (sample_times) MTG_HIP_TRY(ctx, hipMemcpyAsync(sample_times, base + o_st, b_st, hipMemcpyDeviceToHost, ctx->stream));
   }
@@ -359,12 +399,38 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
 }
 
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms) {
-  if (!ctx || !ms) return MTG_ERR_INVALID_ARGUMENT;
+  if (!ms) return MTG_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  int rc = mtg_kernel_times(ctx, ms, 1, &n);
+  if (rc == MTG_OK && n == 0) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "no timed launch yet");
+  return rc;
+}
+
+int mtg_enable_timing(mtg_ctx* ctx, int ring) {
+  if (!ctx || ring < 1) return MTG_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> g(ctx->mu);
-  if (!ctx->timed) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "no timed launch yet");
   MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
-  MTG_HIP_TRY(ctx, hipEventSynchronize(ctx->ev1));
-  MTG_HIP_TRY(ctx, hipEventElapsedTime(ms, ctx->ev0, ctx->ev1));
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  MTG_HIP_TRY(ctx, create_events(ctx, ring));
+  return MTG_OK;
+}
+
+int mtg_kernel_times(mtg_ctx* ctx, float* ms, int n, int* n_out) {
+  if (!ctx || !ms || n < 0 || !n_out) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int64_t ring = (int64_t)ctx->ev_start.size();
+  const int64_t have = std::min<int64_t>(ctx->launches, ring);
+  const int64_t take = std::min<int64_t>(have, n);
+  *n_out = 0;
+  if (take == 0) return MTG_OK;
+  const size_t newest = (size_t)((ctx->launches - 1) % ring);
+  MTG_HIP_TRY(ctx, hipEventSynchronize(ctx->ev_stop[newest]));
+  for (int64_t i = 0; i < take; ++i) {
+    const size_t slot = (size_t)((ctx->launches - take + i) % ring);
+    MTG_HIP_TRY(ctx, hipEventElapsedTime(&ms[i], ctx->ev_start[slot], ctx->ev_stop[slot]));
+  }
+  *n_out = (int)take;
   return MTG_OK;
 }
 

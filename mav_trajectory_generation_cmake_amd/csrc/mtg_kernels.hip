@@ -53,15 +53,27 @@ constexpr int kBlock = 64;
 constexpr size_t kMaxLdsPerBlock = 64 * 1024;
 constexpr size_t kMaxLdsHard = 160 * 1024;
 
-// s[k] = T^k (k < H) and sc = T^(1-2r): the time-scaling of one segment.
-template <int H>
-__device__ __forceinline__ void seg_powers(double T, int r, double (&s)[H], double& sc) {
+// 1/x from v_rcp_f64 plus two Newton steps (full FP64 accuracy; no IEEE division sequence).
+__device__ __forceinline__ double rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = __builtin_fma(-x, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-x, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+
+// s[k] = T^k (k < H) and sc = T^(1-2R) = 1 / (T^R T^(R-1)): the time-scaling of one segment.
+template <int H, int R>
+__device__ __forceinline__ void seg_powers(double T, double (&s)[H], double& sc) {
+  static_assert(R >= 0 && R < H, "derivative_to_optimize must be in [0, N/2-1]");
   s[0] = 1.0;
 #pragma unroll
   for (int k = 1; k < H; ++k) s[k] = s[k - 1] * T;
-  double p = 1.0;
-  for (int i = 0; i < 2 * r - 1; ++i) p *= T;
-  sc = (r == 0) ? T : 1.0 / p;
+  if constexpr (R == 0) {
+    sc = T;
+  } else {
+    sc = rcp(s[R] * s[R - 1]);
+  }
 }
 
 __device__ __forceinline__ bool time_ok(double T) { return T >= DBL_EPSILON && T <= DBL_MAX; }
@@ -77,60 +89,67 @@ __device__ __forceinline__ void load_fixed(const double* vals, int v, int D, int
   }
 }
 
-// Factor the h x h SPD matrix S (lower triangle used) as L L^T; dinv = 1/diag(L).
-// Returns false on a non-positive or non-finite pivot.
+// In-place LU without pivoting of the h x h pivot block (unit-lower L below the diagonal,
+// U on and above it); dinv = 1/diag(U).  The block's fixed rows are identity rows (pivot 1)
+// and its free-free part is the SPD Schur complement of R_pp, so no pivoting is needed.
+// Returns the smallest pivot (<= 0 or non-finite: R_pp not SPD; the reference never checks,
+// lin_impl:355-368).
 template <int H>
-__device__ __forceinline__ bool chol(const double (&S)[H][H], double (&L)[H][H], double (&dinv)[H]) {
-  bool ok = true;
+__device__ __forceinline__ double lu_inplace(double (&S)[H][H], double (&dinv)[H]) {
+  double pmin = DBL_MAX;
 #pragma unroll
-  for (int j = 0; j < H; ++j) {
-    double s = S[j][j];
+  for (int k = 0; k < H; ++k) {
+    const double piv = S[k][k];
+    pmin = fmin(pmin, piv);
+    const double inv = rcp(piv);
+    dinv[k] = inv;
 #pragma unroll
-    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-    ok = ok && (s > 0.0) && (s <= DBL_MAX);
-    const double l = sqrt(s);
-    const double inv = 1.0 / l;
-    L[j][j] = l;
-    dinv[j] = inv;
+    for (int i = k + 1; i < H; ++i) {
+      const double l = S[i][k] * inv;
+      S[i][k] = l;
 #pragma unroll
-    for (int i = j + 1; i < H; ++i) {
-      double t = S[i][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) t -= L[i][k] * L[j][k];
-      L[i][j] = t * inv;
+      for (int j = k + 1; j < H; ++j) S[i][j] -= l * S[k][j];
     }
   }
-  return ok;
+  return pmin;
 }
 
-// x = (L L^T)^-1 b
 template <int H>
-__device__ __forceinline__ void chol_solve(const double (&L)[H][H], const double (&dinv)[H],
-                                           const double (&b)[H], double (&x)[H]) {
+__device__ __forceinline__ void lu_solve(const double (&S)[H][H], const double (&dinv)[H],
+                                         const double (&b)[H], double (&x)[H]) {
   double y[H];
 #pragma unroll
   for (int i = 0; i < H; ++i) {
     double t = b[i];
 #pragma unroll
-    for (int k = 0; k < i; ++k) t -= L[i][k] * y[k];
-    y[i] = t * dinv[i];
+    for (int k = 0; k < i; ++k) t -= S[i][k] * y[k];
+    y[i] = t;
   }
 #pragma unroll
   for (int i = H - 1; i >= 0; --i) {
     double t = y[i];
 #pragma unroll
-    for (int k = i + 1; k < H; ++k) t -= L[k][i] * x[k];
+    for (int k = i + 1; k < H; ++k) t -= S[i][k] * x[k];
     x[i] = t * dinv[i];
   }
 }
 
-// Per-trajectory LDS slot (doubles): exchange buffer, G_v (K x h x h), z_v (V x D x h).
+// Per-trajectory LDS slot (doubles): exchange buffer (LG x h), G_v (K x h x h), Z_v (V x D x h:
+// z_v after the forward sweep, the solution x_v after the backward sweep).
 __host__ __device__ __forceinline__ int slot_doubles(int H, int D, int K, int LG) {
-  const int sb = (H * H > LG ? H * H : LG);
-  return sb + K * H * H + (K + 1) * D * H;
+  return LG * H + K * H * H + (K + 1) * D * H;
 }
 
-template <int N>
+// Re-materialise a uniform table pointer inside a loop so the compiler reloads the table
+// from the scalar cache instead of hoisting 100+ doubles into SGPRs and spilling them.
+typedef const __attribute__((address_space(4))) double cdouble;
+__device__ __forceinline__ cdouble* launder(const double* p) {
+  cdouble* q = (cdouble*)p;
+  asm volatile("" : "+s"(q));
+  return q;
+}
+
+template <int N, int R>
 __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg_log2) {
   constexpr int H = N / 2;
   constexpr unsigned HMASK = (1u << H) - 1u;
@@ -143,227 +162,218 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
   const int tpb = kBlock >> lg_log2;
   const int64_t pair = (int64_t)blockIdx.x * tpb + slot;
   const bool valid = pair < a.B;
-  const int K = a.K, V = K + 1, D = a.D, r = a.r;
+  const int K = a.K, V = K + 1, D = a.D;
   const bool is_g = c < H;
   const bool is_d = (c >= H) && (c < H + D);
   const int d = is_d ? c - H : 0;
-  const int cs = is_g ? c : 0;  // shift amount kept < 32 on non-column lanes
+  const int cs = is_g ? c : 0;
   const int64_t pb = valid ? pair : 0;
   const int64_t tb = pb / a.n_cand;
   const double tscale = a.scales ? a.scales[pb % a.n_cand] : 1.0;
 
-  double* sbuf = lds + (size_t)slot * slot_doubles(H, D, K, LG);
-  const int sb = (H * H > LG ? H * H : LG);
-  double* gst = sbuf + sb;
+  double* xs = lds + (size_t)slot * slot_doubles(H, D, K, LG);
+  double* gst = xs + LG * H;
   double* zst = gst + K * H * H;
 
-  const double* Ht = c_htilde + (MTG_HTILDE_BASE(N) + r * N * N);
-  const double* Ai1 = c_a1inv + MTG_A1INV_OFF(N);
+  const double* Ht = c_htilde + MTG_HTILDE_OFF(N, R);
   const double* vals = a.values + tb * (int64_t)V * H * D;
   const uint8_t* msk = a.mask + tb * V;
   const double* tms = a.times + tb * K;
 
-  int st = 0;
-  int n_free = 0;
-
-  // ---------------- forward block-Thomas sweep over vertices ----------------
-  unsigned raw = msk[0];
-  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned m_cur = raw & HMASK;
-  raw = msk[1];
-  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned m_next = raw & HMASK;
-  double xf_cur[H], xf_next[H], gp[H], wz[H];
-  load_fixed<H>(vals, 0, D, d, m_cur, xf_cur);
-  load_fixed<H>(vals, 1, D, d, m_next, xf_next);
+  // Htilde columns this lane needs as a column owner (lane-varying index: loaded once).
+  double hTL[H], hBR[H], hTR[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) gp[k] = 0.0, wz[k] = 0.0;
-  double T_prev = 0.0, T_next = tms[0] * tscale;
-  if (!time_ok(T_next)) st |= MTG_TRAJ_BAD_TIME;
+  for (int i = 0; i < H; ++i) {
+    hTL[i] = Ht[i * N + cs];
+    hBR[i] = Ht[(H + i) * N + H + cs];
+    hTR[i] = Ht[i * N + H + cs];
+  }
 
+  // ---- forward block-Thomas sweep on the row-pinned system:
+  //   S_v = D_v - C_v G_{v-1},  [G_v | z_v] = S_v^-1 [E_v | b_v - C_v z_{v-1}]
+  // where C_v / E_v are the lower / upper coupling blocks (H_{v-1} bottom-left, H_v top-right)
+  // and fixed rows of S_v, C_v, E_v are replaced by identity / zero rows with the fixed value
+  // in b_v.  Lane c < H owns column c of [E_v | G_v], lane H + d the right-hand side of dim d.
+  int st = 0, n_free = 0;
+  double pmin = DBL_MAX;
+  double gprev[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) gprev[k] = 0.0;
+  double sp[H], scp = 0.0, sn[H], scn = 0.0;
+#pragma unroll
+  for (int k = 0; k < H; ++k) sp[k] = 0.0;
+  {
+    const double T0 = tms[0] * tscale;
+    if (!time_ok(T0)) st |= MTG_TRAJ_BAD_TIME;
+    seg_powers<H, R>(T0, sn, scn);
+  }
+  unsigned raw = msk[0];
   for (int v = 0; v < V; ++v) {
     const bool has_prev = v > 0, has_next = v < K;
-    double a1[H], a2[H], a34[H], m[H], y[H];
-    const bool c_free_cur = !((m_cur >> cs) & 1u);
-    const bool c_free_next = !((m_next >> cs) & 1u);
+    if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
+    const unsigned m_cur = raw & HMASK;
+    if (has_next) raw = msk[v + 1];
+    // w = C_v gprev  (bottom-left block of H_{v-1}; rows masked below)
+    double w[H];
 #pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const double ek = (k == c) ? 1.0 : 0.0;
-      a1[k] = is_g ? (c_free_cur ? ek : 0.0) : xf_cur[k];
-      a2[k] = is_g ? -gp[k] : wz[k];
-      a34[k] = is_g ? (c_free_next ? ek : 0.0) : xf_next[k];
-      m[k] = 0.0;
-      y[k] = 0.0;
-    }
+    for (int i = 0; i < H; ++i) w[i] = 0.0;
     if (has_prev) {
-      // H_{v-1} bottom rows: [BL | BR] . [a2 ; a1]  (E_{v-1}^T a2 + D_v^(prev) a1)
-      double sp[H], scp;
-      seg_powers<H>(T_prev, r, sp, scp);
-      double u[N];
+      double u[H];
 #pragma unroll
-      for (int k = 0; k < H; ++k) u[k] = sp[k] * a2[k], u[H + k] = sp[k] * a1[k];
+      for (int k = 0; k < H; ++k) u[k] = sp[k] * gprev[k];
 #pragma unroll
       for (int i = 0; i < H; ++i) {
-        double acc = 0.0;
+        double t = 0.0;
 #pragma unroll
-        for (int j = 0; j < N; ++j) acc += Ht[(H + i) * N + j] * u[j];
-        m[i] = scp * sp[i] * acc;
+        for (int j = 0; j < H; ++j) t += Ht[(H + i) * N + j] * u[j];
+        w[i] = scp * sp[i] * t;
       }
     }
-    if (has_next) {
-      // H_v top rows: TL . a1 (D_v^(next) a1) and TR . a34 (E_v a34)
-      double sn[H], scn;
-      seg_powers<H>(T_next, r, sn, scn);
-      double w1[H], w3[H];
+    double val[H];
+    {
+      const double* p = vals + ((size_t)v * H) * D + d;
 #pragma unroll
-      for (int k = 0; k < H; ++k) w1[k] = sn[k] * a1[k], w3[k] = sn[k] * a34[k];
-#pragma unroll
-      for (int i = 0; i < H; ++i) {
-        double acc1 = 0.0, acc3 = 0.0;
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          acc1 += Ht[i * N + j] * w1[j];
-          acc3 += Ht[i * N + H + j] * w3[j];
-        }
-        m[i] += scn * sn[i] * acc1;
-        y[i] = scn * sn[i] * acc3;
-      }
+      for (int k = 0; k < H; ++k) val[k] = p[k * D];
     }
-    // Column c of the pinned S_v (G lanes) and the right-hand side.
-    double rhs[H];
+    const double fp = has_prev ? scp * sp[cs] : 0.0;   // column-c factors of the two segments
+    const double fnx = has_next ? scn * sn[cs] : 0.0;
+    double u[H];
 #pragma unroll
     for (int i = 0; i < H; ++i) {
       const bool fi = !((m_cur >> i) & 1u);
-      const double scol = c_free_cur ? (fi ? m[i] : 0.0) : (i == c ? 1.0 : 0.0);
-      rhs[i] = is_g ? (fi ? y[i] : 0.0) : (fi ? -(m[i] + y[i]) : 0.0);
-      if (is_g) sbuf[c * H + i] = scol;
+      const double dcol = fp * sp[i] * hBR[i] + fnx * sn[i] * hTL[i];  // column c of D_v
+      const double ecol = fnx * sn[i] * hTR[i];                        // column c of E_v
+      xs[c * H + i] = fi ? dcol - w[i] : (i == c ? 1.0 : 0.0);         // only c < H is read
+      double ug = fi ? ecol : 0.0;
+      double ud = fi ? -w[i] : val[i];
+      asm volatile("" : "+v"(ug), "+v"(ud));  // both computed: branch-free selects
+      u[i] = is_g ? ug : ud;
     }
     __syncthreads();
     double S[H][H];
 #pragma unroll
     for (int i = 0; i < H; ++i)
 #pragma unroll
-      for (int j = 0; j <= i; ++j) S[i][j] = sbuf[j * H + i];
+      for (int j = 0; j < H; ++j) S[i][j] = xs[j * H + i];
     __syncthreads();
-    double L[H][H], dinv[H], x[H];
-    if (!chol<H>(S, L, dinv)) st |= MTG_TRAJ_NOT_SPD;
-    chol_solve<H>(L, dinv, rhs, x);
+    double dinv[H], x[H];
+    pmin = fmin(pmin, lu_inplace<H>(S, dinv));
+    lu_solve<H>(S, dinv, u, x);
     if (is_g && has_next) {
 #pragma unroll
-      for (int i = 0; i < H; ++i) gst[(v * H + c) * H + i] = x[i], gp[i] = x[i];
+      for (int i = 0; i < H; ++i) gst[(v * H + c) * H + i] = x[i];
     }
     if (is_d) {
 #pragma unroll
-      for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i], wz[i] = xf_cur[i] + x[i];
+      for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i];
     }
+#pragma unroll
+    for (int i = 0; i < H; ++i) gprev[i] = x[i];
     n_free += __builtin_popcount(~m_cur & HMASK);
     if (has_next) {
-      m_cur = m_next;
 #pragma unroll
-      for (int k = 0; k < H; ++k) xf_cur[k] = xf_next[k];
-      T_prev = T_next;
+      for (int k = 0; k < H; ++k) sp[k] = sn[k];
+      scp = scn;
       if (v + 1 < K) {
-        raw = msk[v + 2];
-        if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-        m_next = raw & HMASK;
-        load_fixed<H>(vals, v + 2, D, d, m_next, xf_next);
-        T_next = tms[v + 1] * tscale;
-        if (!time_ok(T_next)) st |= MTG_TRAJ_BAD_TIME;
-      } else {
-        m_next = 0;
-#pragma unroll
-        for (int k = 0; k < H; ++k) xf_next[k] = 0.0;
-        T_next = 0.0;
+        const double Tn = tms[v + 1] * tscale;
+        if (!time_ok(Tn)) st |= MTG_TRAJ_BAD_TIME;
+        seg_powers<H, R>(Tn, sn, scn);
       }
     }
   }
+  if (!(pmin > 0.0 && pmin <= DBL_MAX)) st |= MTG_TRAJ_NOT_SPD;
+  __syncthreads();
 
-  // ------------- backward sweep: x_v, coefficients, free values, cost -------------
-  double cacc = 0.0;
+  // ---- backward substitution (dimension lanes): x_v = z_v - G_v x_{v+1}, kept in Z
   if (is_d) {
-    double xn[H], xfn[H];
+    double xn[H];
 #pragma unroll
-    for (int k = 0; k < H; ++k) xn[k] = 0.0, xfn[k] = 0.0;
-    int idx = n_free;
-    const int64_t fstride = (int64_t)V * H;
-    for (int v = K; v >= 0; --v) {
-      const unsigned mv = msk[v] & HMASK;
-      double x[H], xf[H], xfull[H];
+    for (int k = 0; k < H; ++k) xn[k] = zst[(K * D + d) * H + k];
+    for (int v = K - 1; v >= 0; --v) {
+      double x[H];
 #pragma unroll
       for (int i = 0; i < H; ++i) x[i] = zst[(v * D + d) * H + i];
-      if (v < K) {
 #pragma unroll
-        for (int cc = 0; cc < H; ++cc) {
-          const double xc = xn[cc];
+      for (int cc = 0; cc < H; ++cc) {
+        const double xc = xn[cc];
 #pragma unroll
-          for (int i = 0; i < H; ++i) x[i] -= gst[(v * H + cc) * H + i] * xc;
-        }
-      }
-      load_fixed<H>(vals, v, D, d, mv, xf);
-#pragma unroll
-      for (int i = 0; i < H; ++i) xfull[i] = x[i] + xf[i];
-      if (v < K) {
-        const double T = tms[v] * tscale;
-        double s[H], sc;
-        seg_powers<H>(T, r, s, sc);
-        double sh[N];
-#pragma unroll
-        for (int k = 0; k < H; ++k) sh[k] = s[k] * xfull[k], sh[H + k] = s[k] * xfn[k];
-        if (a.coeffs) {
-          // c = diag(T^-j) A(1)^-1 (S [x_v; x_{v+1}]); A(1)^-1 top-left = diag(1/k!), top-right = 0
-          const double tinv = 1.0 / T;
-          double out[N];
-          double tp = 1.0;
-#pragma unroll
-          for (int j = 0; j < N; ++j) {
-            double acc;
-            if (j < H) {
-              acc = Ai1[j * N + j] * sh[j];
-            } else {
-              acc = 0.0;
-#pragma unroll
-              for (int q = 0; q < N; ++q) acc += Ai1[j * N + q] * sh[q];
-            }
-            out[j] = acc * tp;
-            tp *= tinv;
-          }
-          if (valid) {
-            double2* dst = reinterpret_cast<double2*>(a.coeffs + ((pb * K + v) * D + d) * N);
-#pragma unroll
-            for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(out[2 * j], out[2 * j + 1]);
-          }
-        }
-        if (a.cost_out) {
-          double q = 0.0;
-#pragma unroll
-          for (int i = 0; i < N; ++i) {
-            double row = 0.0;
-#pragma unroll
-            for (int j = 0; j < N; ++j) row += Ht[i * N + j] * sh[j];
-            q += sh[i] * row;
-          }
-          cacc += sc * q;
-        }
-      }
-      if (a.free_out && valid) {
-        double* fo = a.free_out + (pb * D + d) * fstride;
-#pragma unroll
-        for (int k = H - 1; k >= 0; --k)
-          if (!((mv >> k) & 1u)) fo[--idx] = x[k];
+        for (int i = 0; i < H; ++i) x[i] -= gst[(v * H + cc) * H + i] * xc;
       }
 #pragma unroll
-      for (int k = 0; k < H; ++k) xn[k] = x[k], xfn[k] = xfull[k];
+      for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i], xn[i] = x[i];
     }
   }
-  // cost: sum over dimensions in a fixed order (deterministic)
-  if (a.cost_out) {
+  __syncthreads();
+
+  // ---- epilogue: coefficients c = diag(T^-j) A(1)^-1 S(T) [x_i; x_{i+1}] and the cost, items (i, d)
+  double cacc = 0.0;
+  for (int it = c; it < K * D; it += LG) {
+    const int i = it / D, dd = it - i * D;
+    cdouble* Hl = launder(c_htilde + MTG_HTILDE_OFF(N, R));
+    cdouble* Ai1 = launder(c_a1inv + MTG_A1INV_OFF(N));
+    const double T = tms[i] * tscale;
+    double s[H], sc;
+    seg_powers<H, R>(T, s, sc);
+    double sh[N];
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+      sh[k] = s[k] * zst[(i * D + dd) * H + k];
+      sh[H + k] = s[k] * zst[((i + 1) * D + dd) * H + k];
+    }
+    if (a.coeffs) {
+      const double tinv = rcp(T);
+      double out[N];
+      double tp = 1.0;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        double acc;
+        if (j < H) {  // A(1)^-1 top-left = diag(1/j!), top-right = 0
+          acc = Ai1[j * N + j] * sh[j];
+        } else {
+          acc = 0.0;
+#pragma unroll
+          for (int q = 0; q < N; ++q) acc += Ai1[j * N + q] * sh[q];
+        }
+        out[j] = acc * tp;
+        tp *= tinv;
+      }
+      if (valid) {
+        double2* dst = reinterpret_cast<double2*>(a.coeffs + ((pb * K + i) * D + dd) * N);
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(out[2 * j], out[2 * j + 1]);
+      }
+    }
+    if (a.cost_out) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh
+      double q = 0.0;
+#pragma unroll
+      for (int p = 0; p < N; ++p) {
+        double row = 0.5 * Hl[p * N + p] * sh[p];
+#pragma unroll
+        for (int t = p + 1; t < N; ++t) row += Hl[p * N + t] * sh[t];
+        q += sh[p] * row;
+      }
+      cacc += sc * q;
+    }
+  }
+  // free derivatives in the reference order (sorted by vertex, then derivative)
+  if (a.free_out && valid && is_d) {
+    double* fo = a.free_out + (pb * D + d) * ((int64_t)V * H);
+    int idx = 0;
+    for (int v = 0; v < V; ++v) {
+      const unsigned mv = msk[v] & HMASK;
+#pragma unroll
+      for (int k = 0; k < H; ++k)
+        if (!((mv >> k) & 1u)) fo[idx++] = zst[(v * D + d) * H + k];
+    }
+  }
+  if (a.cost_out) {  // fixed-order reduction over the group's lanes (deterministic)
     __syncthreads();
-    if (is_d) sbuf[d] = cacc;
+    xs[c] = cacc;
     __syncthreads();
-    if (c == H && valid) {
+    if (c == 0 && valid) {
       double tot = 0.0;
-      for (int q = 0; q < D; ++q) tot += sbuf[q];
-      a.cost_out[pb] = 0.5 * tot;
+      for (int q = 0; q < LG; ++q) tot += xs[q];
+      a.cost_out[pb] = tot;
     }
   }
   if (c == 0 && valid) {
@@ -391,8 +401,8 @@ bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes,
   }
 }
 
-template <int N>
-static hipError_t launch_fused_n(const SolveArgs& a, hipStream_t stream) {
+template <int N, int R>
+static hipError_t launch_fused_nr(const SolveArgs& a, hipStream_t stream) {
   int lg, tpb;
   size_t lds;
   if (!solve_geometry(N, a.D, a.K, &lg, &lds, &tpb)) return hipErrorInvalidValue;
@@ -401,12 +411,26 @@ static hipError_t launch_fused_n(const SolveArgs& a, hipStream_t stream) {
   const int64_t blocks = (a.B + tpb - 1) / tpb;
   if (blocks == 0) return hipSuccess;
   if (lds > kMaxLdsPerBlock) {
-    hipError_t e = hipFuncSetAttribute((const void*)solve_fused_kernel<N>,
+    hipError_t e = hipFuncSetAttribute((const void*)solve_fused_kernel<N, R>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(solve_fused_kernel<N>, dim3((unsigned)blocks), dim3(kBlock), lds, stream, a, lg_log2);
+  hipLaunchKernelGGL((solve_fused_kernel<N, R>), dim3((unsigned)blocks), dim3(kBlock), lds, stream, a, lg_log2);
   return hipGetLastError();
+}
+
+template <int N>
+static hipError_t launch_fused_n(const SolveArgs& a, hipStream_t stream) {
+  switch (a.r) {
+    case 0: return launch_fused_nr<N, 0>(a, stream);
+    case 1: if constexpr (N / 2 > 1) return launch_fused_nr<N, 1>(a, stream); break;
+    case 2: if constexpr (N / 2 > 2) return launch_fused_nr<N, 2>(a, stream); break;
+    case 3: if constexpr (N / 2 > 3) return launch_fused_nr<N, 3>(a, stream); break;
+    case 4: if constexpr (N / 2 > 4) return launch_fused_nr<N, 4>(a, stream); break;
+    case 5: if constexpr (N / 2 > 5) return launch_fused_nr<N, 5>(a, stream); break;
+    default: break;
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream) {

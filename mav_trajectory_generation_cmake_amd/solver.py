@@ -55,8 +55,13 @@ class Context:
         self.close()
 
     def set_stream(self, stream_handle):
-        """stream_handle: an int hipStream_t (e.g. torch.cuda.current_stream().cuda_stream) or None."""
-        nat.check(self._lib.mtg_set_stream(self.handle, stream_handle), self.handle)
+        """Launch on this hipStream_t (an int, e.g. torch.cuda.current_stream().cuda_stream);
+        0 / None is the HIP null stream (torch's default stream)."""
+        nat.check(self._lib.mtg_set_stream(self.handle, stream_handle or None), self.handle)
+
+    def reset_stream(self):
+        """Launch on the context's own stream again."""
+        nat.check(self._lib.mtg_reset_stream(self.handle), self.handle)
 
     def synchronize(self):
         nat.check(self._lib.mtg_synchronize(self.handle), self.handle)
@@ -65,6 +70,37 @@ class Context:
         ms = ctypes.c_float(0)
         nat.check(self._lib.mtg_last_kernel_ms(self.handle, ctypes.byref(ms)), self.handle)
         return ms.value
+
+    def enable_timing(self, ring):
+        """Record a HIP event pair around each of the last `ring` kernel launches."""
+        nat.check(self._lib.mtg_enable_timing(self.handle, ring), self.handle)
+
+    def kernel_times_ms(self, n):
+        """Durations (ms) of up to n most recent launches, oldest first (synchronizes)."""
+        buf = (ctypes.c_float * max(n, 1))()
+        got = ctypes.c_int(0)
+        nat.check(self._lib.mtg_kernel_times(self.handle, buf, n, ctypes.byref(got)), self.handle)
+        return np.array(buf[:got.value], dtype=np.float64)
+
+    def solve_call(self, N, r, values, mask, times, coeffs, free=None, n_free=None, cost=None, status=None,
+                   split=False):
+        """A zero-argument callable that launches one device-pointer solve asynchronously on the
+        current stream with the arguments bound once (the bench's step; minimal host overhead)."""
+        import torch
+        B, V, h, D = values.shape
+        K = V - 1
+        self.set_stream(torch.cuda.current_stream(values.device).cuda_stream)
+        flags = nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC | (nat.MTG_FLAG_SPLIT_KERNELS if split else 0)
+        fn = self._lib.mtg_solve_linear_batch
+        args = (self.handle, N, D, K, r, B, _addr(values), _addr(mask), _addr(times), _addr(coeffs), _addr(free),
+                _addr(n_free), _addr(cost), _addr(status), flags)
+        handle = self.handle
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                nat.check(rc, handle)
+        return call
 
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
@@ -108,6 +144,7 @@ class Context:
             values = np.ascontiguousarray(values, dtype=np.float64)
             mask = np.ascontiguousarray(mask, dtype=np.uint8)
             times = np.ascontiguousarray(times, dtype=np.float64)
+            self.reset_stream()
         if split:
             flags |= nat.MTG_FLAG_SPLIT_KERNELS
         rc = self._lib.mtg_solve_linear_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
@@ -134,6 +171,7 @@ class Context:
             scales = np.ascontiguousarray(scales, dtype=np.float64)
             cost = cost if cost is not None else np.empty((B, C))
             flags = 0
+            self.reset_stream()
         rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                             _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
         nat.check(rc, self.handle)
@@ -146,6 +184,7 @@ class Context:
         times = np.ascontiguousarray(times, dtype=np.float64)
         B, K, D, N = coeffs.shape
         counts = np.zeros(B, dtype=np.int64)
+        self.reset_stream()
         nat.check(self._lib.mtg_evaluate_range_batch(self.handle, N, D, K, B, None, _addr(times), t_start, t_end,
                                                      dt, derivative, _addr(counts), None, None, None, 0),
                   self.handle)

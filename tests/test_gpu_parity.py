@@ -32,6 +32,9 @@ def test_golden_truth(gpu_ctx, case):
     assert np.all(out["status"] & 0xFF == 0), out["status"]
     err = scale_normalised_error(out["coeffs"], g["coeffs"], g["times"])
     assert err <= TRUTH_TOL, (case, err)
+    # north_star's "1e-6 relative on the recovered coefficients", element-wise, on every
+    # coefficient that matters (|c_k| T^k >= 1e-4 of the segment's scale), against truth
+    assert masked_elementwise_rel(out["coeffs"], g["coeffs"], g["times"], floor=1e-4) <= 1e-6, case
     np.testing.assert_array_equal(out["n_free"], g["n_free"])
     rel_cost = np.max(np.abs(out["cost"] - g["cost"]) / np.maximum(np.abs(g["cost"]), 1e-300))
     assert rel_cost <= 1e-9, (case, rel_cost)
@@ -72,18 +75,27 @@ def test_vs_oracle_bench_generator(gpu_ctx):
     ref, cost = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times, want_cost=True)
     err = scale_normalised_error(out["coeffs"], ref, times)
     assert err <= ORACLE_TOL_N10, err
-    assert masked_elementwise_rel(out["coeffs"], ref, times) <= 1e-5
+    # element-wise relative error against the FP64 reference algorithm is dominated by the
+    # reference's own rounding (1.7e-5 vs 60-digit truth on cfg2, tests/test_oracle.py), so it is
+    # not a gate here; the element-wise 1e-6 gate is against truth (test_golden_truth).
     assert np.max(np.abs(out["cost"] - cost) / np.abs(cost)) <= 1e-6
 
 
 def test_full_size_invariants(gpu_ctx):
-    """B = 1e4 (config 2): checkPath invariants (abs 1e-6, :73-131) on every trajectory."""
+    """B = 1e4 (config 2): checkPath invariants (:73-131) on every trajectory, and the whole batch
+    against the oracle.  The bench generator draws segment lengths from U(0, 10) m, so a few
+    trajectories have millisecond segments with derivatives of 1e8+: the invariant is checked
+    relative to the trajectory's derivative scale (the reference path itself reaches 5e-7 there,
+    and misses the absolute 1e-6 of :75 by 8e-3)."""
+    O = _oracle()
     B = 10000
     vals, mask, times = _bench_batch(B, seed0=0)
     out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True)
     assert np.all(out["status"] == 0)
-    assert check_path(vals, mask, times, out["coeffs"], 10) < 1e-6
     assert np.all(np.isfinite(out["coeffs"]))
+    assert check_path(vals, mask, times, out["coeffs"], 10, relative=True) < 1e-8
+    ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
+    assert scale_normalised_error(out["coeffs"], ref, times) <= ORACLE_TOL_N10
 
 
 def test_deterministic_and_device_pointers(gpu_ctx):
@@ -148,7 +160,7 @@ def test_segment_counts_vs_oracle(gpu_ctx, K):
     assert np.all(out["status"] == 0)
     ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
     assert scale_normalised_error(out["coeffs"], ref, times) <= 1e-6
-    assert check_path(vals, mask, times, out["coeffs"], 10) < 1e-6
+    assert check_path(vals, mask, times, out["coeffs"], 10, relative=True) < 1e-8
 
 
 def test_time_sweep_matches_solves(gpu_ctx):
