@@ -51,6 +51,22 @@ def traffic_from_profiles(kernel_prefix, batch):
         return None
 
 
+def shard_seed0(rank, batch_per_rank):
+    """Rank r solves trajectories with seeds r*B .. r*B+B-1: contiguous shards of one global
+    batch of world*B independent problems (no data-path exchange)."""
+    return rank * batch_per_rank
+
+
+def max_over_ranks(x, dist, device):
+    """Slowest rank's elapsed time (the job's wall clock); identity at world size 1."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(values, mask, times, N, r, target_s, threads):
     """Oracle (faithful C restatement of lin_impl, dense QR in place of SparseQR) on host cores."""
     from oracle import pyoracle
@@ -98,7 +114,7 @@ def main():
 
     N, K, D, r = args.N, args.segments, 3, 4
     B = args.batch
-    values, mask, times = mtg.random_vertices_path_batch(N, D, K, B, seed0=rank * B)
+    values, mask, times = mtg.random_vertices_path_batch(N, D, K, B, seed0=shard_seed0(rank, B))
     v_d = torch.from_numpy(values).to(dev)
     m_d = torch.from_numpy(mask).to(dev)
     t_d = torch.from_numpy(times).to(dev)
@@ -130,10 +146,7 @@ def main():
     per_launch = ctx.kernel_times_ms(args.steps)
     kern_ms = float(np.mean(per_launch))
     gpu_ms = g0.elapsed_time(g1)
-    tmax = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    el = float(tmax.item())
+    el = max_over_ranks(el, dist if world > 1 else None, dev)
 
     # spot check of the timed outputs (finite, constraint continuity) -- not timed
     c = c_d.cpu().numpy()

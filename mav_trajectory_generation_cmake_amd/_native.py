@@ -80,6 +80,35 @@ class MTGError(RuntimeError):
         self.code = code
 
 
+def hip_runtimes_mapped():
+    """Paths of the libamdhip64 images mapped into this process (Linux)."""
+    found = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1]
+                if "libamdhip64.so" in os.path.basename(p):
+                    found.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return sorted(found)
+
+
+def _share_torch_runtime():
+    """PyTorch-ROCm wheels bundle their own libamdhip64 (soname libamdhip64.so.7, the
+    same as /opt/rocm's).  Loading torch first makes the dynamic linker bind libmtg's
+    libamdhip64.so.7 dependency to torch's already-loaded copy, so the process has ONE
+    HIP runtime: torch stream handles and allocations are then valid in libmtg.  Loading
+    libmtg first would map /opt/rocm's runtime and torch would later map a second one,
+    whose streams/devices libmtg cannot see.  Set MTG_NO_TORCH=1 to skip (torch-free use)."""
+    if os.environ.get("MTG_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path=None):
     """Load libmtg.so; raises if it has not been built (no fallback)."""
     global _lib
@@ -88,6 +117,7 @@ def load(path=None):
     p = path or os.environ.get("MTG_LIBRARY", LIB_PATH)
     if not os.path.exists(p):
         raise MTGError(MTG_ERR_NO_DEVICE, "libmtg.so not found at %s: run __graft_entry__.build()" % p)
+    _share_torch_runtime()
     lib = ctypes.CDLL(p)
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name)

@@ -66,6 +66,9 @@ template <int N>
 __global__ void eval_range_kernel(int D, int K, int64_t B, const double* coeffs, const double* times,
                                   double t_start, double t_end, double dt, int derivative,
                                   const int64_t* offsets, double* out, double* sample_times) {
+  // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
+  // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
+#pragma clang fp contract(off)
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const double* tms = times + b * K;
@@ -88,12 +91,16 @@ __global__ void eval_range_kernel(int D, int K, int64_t B, const double* coeffs,
       double v = 0.0;
       if (derivative < N) {
         const double* c = cs + d * N;
-        // result = row[N-1] c[N-1]; result *= t; result += row[j] c[j]  (no FMA contraction,
-        // so the rounding is the reference's multiply-then-add)
-        v = __dmul_rn(row[N - 1], c[N - 1]);
+        // result = row[N-1] c[N-1]; result *= t; result += row[j] c[j]: plain operators under
+        // the contract(off) pragma above, so the rounding is the reference's multiply-then-add
+        // (the pragma does not reach into inlined helpers such as __dmul_rn)
+        v = row[N - 1] * c[N - 1];
 #pragma unroll
         for (int j = N - 2; j >= 0; --j) {
-          if (j >= derivative) v = __dadd_rn(__dmul_rn(v, tin), __dmul_rn(row[j], c[j]));
+          if (j >= derivative) {
+            v = v * tin;
+            v = v + row[j] * c[j];
+          }
         }
       }
       out[n * D + d] = v;

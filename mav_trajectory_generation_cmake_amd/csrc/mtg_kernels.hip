@@ -42,6 +42,7 @@
 #include "mtg_tables.inc"
 
 #include <float.h>
+#include <stdlib.h>
 
 namespace mtg {
 
@@ -55,6 +56,9 @@ constexpr size_t kMaxLdsHard = 160 * 1024;
 
 // 1/x from v_rcp_f64 plus two Newton steps (full FP64 accuracy; no IEEE division sequence).
 __device__ __forceinline__ double rcp(double x) {
+#ifdef MTG_IEEE_DIV
+  return 1.0 / x;
+#endif
   double y = __builtin_amdgcn_rcp(x);
   double e = __builtin_fma(-x, y, 1.0);
   y = __builtin_fma(y, e, y);
@@ -89,34 +93,41 @@ __device__ __forceinline__ void load_fixed(const double* vals, int v, int D, int
   }
 }
 
-// In-place LU without pivoting of the h x h pivot block (unit-lower L below the diagonal,
-// U on and above it); dinv = 1/diag(U).  The block's fixed rows are identity rows (pivot 1)
-// and its free-free part is the SPD Schur complement of R_pp, so no pivoting is needed.
-// Returns the smallest pivot (<= 0 or non-finite: R_pp not SPD; the reference never checks,
-// lin_impl:355-368).
+// S = L diag(d) L^T (L unit lower, below the diagonal of S; only the lower triangle of S is
+// read); dinv = 1/d.  Returns the smallest pivot (<= 0 or non-finite: R_pp is not SPD; the
+// reference never checks, lin_impl:355-368).
 template <int H>
-__device__ __forceinline__ double lu_inplace(double (&S)[H][H], double (&dinv)[H]) {
+__device__ __forceinline__ double ldlt(double (&S)[H][H], double (&dinv)[H]) {
   double pmin = DBL_MAX;
+  double dg[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    const double piv = S[k][k];
-    pmin = fmin(pmin, piv);
-    const double inv = rcp(piv);
-    dinv[k] = inv;
+  for (int j = 0; j < H; ++j) {
+    double w[H];
+    double dj = S[j][j];
 #pragma unroll
-    for (int i = k + 1; i < H; ++i) {
-      const double l = S[i][k] * inv;
-      S[i][k] = l;
+    for (int k = 0; k < j; ++k) {
+      w[k] = S[j][k] * dg[k];
+      dj -= S[j][k] * w[k];
+    }
+    pmin = dj < pmin ? dj : pmin;
+    const double inv = rcp(dj);
+    dg[j] = dj;
+    dinv[j] = inv;
 #pragma unroll
-      for (int j = k + 1; j < H; ++j) S[i][j] -= l * S[k][j];
+    for (int i = j + 1; i < H; ++i) {
+      double t = S[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= S[i][k] * w[k];
+      S[i][j] = t * inv;
     }
   }
   return pmin;
 }
 
+// x = S^-1 b with S factored in place by ldlt()
 template <int H>
-__device__ __forceinline__ void lu_solve(const double (&S)[H][H], const double (&dinv)[H],
-                                         const double (&b)[H], double (&x)[H]) {
+__device__ __forceinline__ void ldlt_solve(const double (&S)[H][H], const double (&dinv)[H],
+                                           const double (&b)[H], double (&x)[H]) {
   double y[H];
 #pragma unroll
   for (int i = 0; i < H; ++i) {
@@ -127,15 +138,15 @@ __device__ __forceinline__ void lu_solve(const double (&S)[H][H], const double (
   }
 #pragma unroll
   for (int i = H - 1; i >= 0; --i) {
-    double t = y[i];
+    double t = y[i] * dinv[i];
 #pragma unroll
-    for (int k = i + 1; k < H; ++k) t -= S[i][k] * x[k];
-    x[i] = t * dinv[i];
+    for (int k = i + 1; k < H; ++k) t -= S[k][i] * x[k];
+    x[i] = t;
   }
 }
 
 // Per-trajectory LDS slot (doubles): exchange buffer (LG x h), G_v (K x h x h), Z_v (V x D x h:
-// z_v after the forward sweep, the solution x_v after the backward sweep).
+// z_v after the forward sweep, the pinned solution x_v after the backward sweep).
 __host__ __device__ __forceinline__ int slot_doubles(int H, int D, int K, int LG) {
   return LG * H + K * H * H + (K + 1) * D * H;
 }
@@ -180,25 +191,18 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
   const uint8_t* msk = a.mask + tb * V;
   const double* tms = a.times + tb * K;
 
-  // Htilde columns this lane needs as a column owner (lane-varying index: loaded once).
-  double hTL[H], hBR[H], hTR[H];
-#pragma unroll
-  for (int i = 0; i < H; ++i) {
-    hTL[i] = Ht[i * N + cs];
-    hBR[i] = Ht[(H + i) * N + H + cs];
-    hTR[i] = Ht[i * N + H + cs];
-  }
-
-  // ---- forward block-Thomas sweep on the row-pinned system:
-  //   S_v = D_v - C_v G_{v-1},  [G_v | z_v] = S_v^-1 [E_v | b_v - C_v z_{v-1}]
-  // where C_v / E_v are the lower / upper coupling blocks (H_{v-1} bottom-left, H_v top-right)
-  // and fixed rows of S_v, C_v, E_v are replaced by identity / zero rows with the fixed value
-  // in b_v.  Lane c < H owns column c of [E_v | G_v], lane H + d the right-hand side of dim d.
+  // ---- forward block-Thomas sweep on the symmetrically pinned system (fixed rows AND columns
+  // of R replaced by the identity, fixed values moved to the right-hand side):
+  //   S_v = D_v - E_{v-1}^T G_{v-1},  [G_v | z_v] = S_v^-1 [E_v | rhs_v],
+  //   rhs_v = -(D_v xf_v + E_{v-1}^T (xf_{v-1} + z_{v-1}) + E_v xf_{v+1})   (free rows).
+  // Every lane runs the same four mat-vecs against Htilde per vertex with its own inputs:
+  //   column lane c:  a1 = e_c (column c of D_v), a2 = -g_{v-1}, a3 = e_c (column c of E_v)
+  //   dim lane d:     a1 = xf_v, a2 = xf_{v-1} + z_{v-1}, a3 = xf_{v+1}
   int st = 0, n_free = 0;
   double pmin = DBL_MAX;
-  double gprev[H];
+  double gp[H], xfc[H], xfn[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) gprev[k] = 0.0;
+  for (int k = 0; k < H; ++k) gp[k] = 0.0;
   double sp[H], scp = 0.0, sn[H], scn = 0.0;
 #pragma unroll
   for (int k = 0; k < H; ++k) sp[k] = 0.0;
@@ -208,57 +212,99 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
     seg_powers<H, R>(T0, sn, scn);
   }
   unsigned raw = msk[0];
+  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
+  unsigned m_cur = raw & HMASK;
+  raw = msk[1];
+  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
+  unsigned m_next = raw & HMASK;
+  unsigned m_prev = 0;
+  double xfp0 = 0.0;  // fixed position of vertex v-1 (dim lanes)
+  load_fixed<H>(vals, 0, D, d, m_cur, xfc);
+  load_fixed<H>(vals, 1, D, d, m_next, xfn);
   for (int v = 0; v < V; ++v) {
     const bool has_prev = v > 0, has_next = v < K;
-    if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-    const unsigned m_cur = raw & HMASK;
-    if (has_next) raw = msk[v + 1];
-    // w = C_v gprev  (bottom-left block of H_{v-1}; rows masked below)
-    double w[H];
+    cdouble* Hs = launder(Ht);
+    const bool c_free = !((m_cur >> cs) & 1u);
+    const bool c_free_next = !((m_next >> cs) & 1u);
+    double a1[H], a2[H], a3[H];
 #pragma unroll
-    for (int i = 0; i < H; ++i) w[i] = 0.0;
-    if (has_prev) {
-      double u[H];
+    for (int k = 0; k < H; ++k) {
+      const double ek = (k == c) ? 1.0 : 0.0;
+      a1[k] = is_g ? (c_free ? ek : 0.0) : xfc[k];
+      a2[k] = gp[k];  // column lanes keep -g_{v-1}, dim lanes xf_{v-1} + z_{v-1}
+      a3[k] = is_g ? (c_free_next ? ek : 0.0) : xfn[k];
+    }
+    // Translation invariance (r >= 1: H_i [1 0..0 1 0..0]^T = 0): for a segment whose two end
+    // positions are both fixed, the fixed-value products use positions relative to the segment
+    // start.  Exact in real arithmetic; in FP64 it removes the cancellation of
+    // H^TL p_v + H^TR p_{v+1} on short segments (up to 500x more accurate, DESIGN.md "Numerics").
+    double a1b0 = a1[0];
+    if (R >= 1 && is_d) {
+      const bool pos_c = m_cur & 1u, pos_p = m_prev & 1u, pos_n = m_next & 1u;
+      if (has_prev && pos_p && pos_c) {  // segment v-1: positions relative to p_{v-1}
+        a1b0 = xfc[0] - xfp0;
+        a2[0] = 0.0;
+      }
+      if (has_next && pos_c && pos_n) {  // segment v: positions relative to p_v
+        a3[0] = xfn[0] - xfc[0];
+        a1[0] = 0.0;
+      }
+    }
+    double m[H], y[H];
 #pragma unroll
-      for (int k = 0; k < H; ++k) u[k] = sp[k] * gprev[k];
+    for (int i = 0; i < H; ++i) m[i] = 0.0, y[i] = 0.0;
+    if (has_prev) {  // bottom rows of H_{v-1}: [BL | BR] [a2; a1]
+      double u[N];
+#pragma unroll
+      for (int k = 0; k < H; ++k) u[k] = sp[k] * a2[k], u[H + k] = sp[k] * a1[k];
+      u[H] = a1b0;  // sp[0] == 1
 #pragma unroll
       for (int i = 0; i < H; ++i) {
         double t = 0.0;
 #pragma unroll
-        for (int j = 0; j < H; ++j) t += Ht[(H + i) * N + j] * u[j];
-        w[i] = scp * sp[i] * t;
+        for (int j = 0; j < N; ++j) t += Hs[(H + i) * N + j] * u[j];
+        m[i] = scp * sp[i] * t;
       }
     }
-    double val[H];
-    {
-      const double* p = vals + ((size_t)v * H) * D + d;
+    if (has_next) {  // top rows of H_v: TL a1 and TR a3
+      double w1[H], w3[H];
 #pragma unroll
-      for (int k = 0; k < H; ++k) val[k] = p[k * D];
+      for (int k = 0; k < H; ++k) w1[k] = sn[k] * a1[k], w3[k] = sn[k] * a3[k];
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        double t1 = 0.0, t3 = 0.0;
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+          t1 += Hs[i * N + j] * w1[j];
+          t3 += Hs[i * N + H + j] * w3[j];
+        }
+        const double f = scn * sn[i];
+        m[i] += f * t1;
+        y[i] = f * t3;
+      }
     }
-    const double fp = has_prev ? scp * sp[cs] : 0.0;   // column-c factors of the two segments
-    const double fnx = has_next ? scn * sn[cs] : 0.0;
-    double u[H];
+    double rhs[H];
 #pragma unroll
     for (int i = 0; i < H; ++i) {
       const bool fi = !((m_cur >> i) & 1u);
-      const double dcol = fp * sp[i] * hBR[i] + fnx * sn[i] * hTL[i];  // column c of D_v
-      const double ecol = fnx * sn[i] * hTR[i];                        // column c of E_v
-      xs[c * H + i] = fi ? dcol - w[i] : (i == c ? 1.0 : 0.0);         // only c < H is read
-      double ug = fi ? ecol : 0.0;
-      double ud = fi ? -w[i] : val[i];
-      asm volatile("" : "+v"(ug), "+v"(ud));  // both computed: branch-free selects
-      u[i] = is_g ? ug : ud;
+      double sv = c_free ? (fi ? m[i] : 0.0) : (i == c ? 1.0 : 0.0);
+      double rg = fi ? y[i] : 0.0;
+      double rd = fi ? -(m[i] + y[i]) : 0.0;
+      asm volatile("" : "+v"(sv), "+v"(rg), "+v"(rd));  // all computed: branch-free selects
+      xs[c * H + i] = sv;  // only columns c < H are read
+      rhs[i] = is_g ? rg : rd;
     }
     __syncthreads();
     double S[H][H];
 #pragma unroll
     for (int i = 0; i < H; ++i)
 #pragma unroll
-      for (int j = 0; j < H; ++j) S[i][j] = xs[j * H + i];
+      for (int j = 0; j <= i; ++j) S[i][j] = xs[j * H + i];
     __syncthreads();
     double dinv[H], x[H];
-    pmin = fmin(pmin, lu_inplace<H>(S, dinv));
-    lu_solve<H>(S, dinv, u, x);
+    const double pv = ldlt<H>(S, dinv);
+    pmin = pv < pmin ? pv : pmin;
+    ldlt_solve<H>(S, dinv, rhs, x);
     if (is_g && has_next) {
 #pragma unroll
       for (int i = 0; i < H; ++i) gst[(v * H + c) * H + i] = x[i];
@@ -268,16 +314,27 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
       for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i];
     }
 #pragma unroll
-    for (int i = 0; i < H; ++i) gprev[i] = x[i];
+    for (int i = 0; i < H; ++i) gp[i] = is_g ? -x[i] : xfc[i] + x[i];
     n_free += __builtin_popcount(~m_cur & HMASK);
     if (has_next) {
+      xfp0 = xfc[0];
+      m_prev = m_cur;
 #pragma unroll
-      for (int k = 0; k < H; ++k) sp[k] = sn[k];
+      for (int k = 0; k < H; ++k) sp[k] = sn[k], xfc[k] = xfn[k];
       scp = scn;
+      m_cur = m_next;
       if (v + 1 < K) {
         const double Tn = tms[v + 1] * tscale;
         if (!time_ok(Tn)) st |= MTG_TRAJ_BAD_TIME;
         seg_powers<H, R>(Tn, sn, scn);
+        raw = msk[v + 2];
+        if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
+        m_next = raw & HMASK;
+        load_fixed<H>(vals, v + 2, D, d, m_next, xfn);
+      } else {
+        m_next = 0;
+#pragma unroll
+        for (int k = 0; k < H; ++k) xfn[k] = 0.0;
       }
     }
   }
@@ -314,12 +371,20 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
     const double T = tms[i] * tscale;
     double s[H], sc;
     seg_powers<H, R>(T, s, sc);
+    double x0[H], x1[H];
+    load_fixed<H>(vals, i, D, dd, msk[i], x0);
+    load_fixed<H>(vals, i + 1, D, dd, msk[i + 1], x1);
     double sh[N];
 #pragma unroll
     for (int k = 0; k < H; ++k) {
-      sh[k] = s[k] * zst[(i * D + dd) * H + k];
-      sh[H + k] = s[k] * zst[((i + 1) * D + dd) * H + k];
+      sh[k] = s[k] * (x0[k] + zst[(i * D + dd) * H + k]);
+      sh[H + k] = s[k] * (x1[k] + zst[((i + 1) * D + dd) * H + k]);
     }
+    // the polynomial of [x_i - p 1; x_{i+1} - p 1] is p(t) - p: recover it relative to the start
+    // position p (only c_0 changes), which avoids cancelling p_i against p_{i+1} in c_j, j >= h
+    const double p0 = sh[0];
+    sh[0] = 0.0;
+    sh[H] -= p0;
     if (a.coeffs) {
       const double tinv = rcp(T);
       double out[N];
@@ -328,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
       for (int j = 0; j < N; ++j) {
         double acc;
         if (j < H) {  // A(1)^-1 top-left = diag(1/j!), top-right = 0
-          acc = Ai1[j * N + j] * sh[j];
+          acc = (j == 0) ? p0 : Ai1[j * N + j] * sh[j];
         } else {
           acc = 0.0;
 #pragma unroll
@@ -343,7 +408,8 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
         for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(out[2 * j], out[2 * j + 1]);
       }
     }
-    if (a.cost_out) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh
+    if (a.cost_out) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)
+      if (R == 0) sh[0] = p0, sh[H] += p0;
       double q = 0.0;
 #pragma unroll
       for (int p = 0; p < N; ++p) {
@@ -410,6 +476,11 @@ static hipError_t launch_fused_nr(const SolveArgs& a, hipStream_t stream) {
   while ((1 << lg_log2) < lg) ++lg_log2;
   const int64_t blocks = (a.B + tpb - 1) / tpb;
   if (blocks == 0) return hipSuccess;
+  static const size_t lds_pad = [] {  // occupancy experiments only (DESIGN.md "Occupancy")
+    const char* p = getenv("MTG_DEBUG_LDS_PAD");
+    return p ? (size_t)atoi(p) : (size_t)0;
+  }();
+  lds += lds_pad;
   if (lds > kMaxLdsPerBlock) {
     hipError_t e = hipFuncSetAttribute((const void*)solve_fused_kernel<N, R>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -1,0 +1,117 @@
+"""CPU tests of the drop-in boundary (include/mtg.h <-> libmtg.so <-> _native.py).
+
+No compute calls here: these run without a GPU and check that the C ABI library
+loads, exports exactly what the header declares, validates arguments and
+reports "no device" loudly (there is no CPU fallback in the product path)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from mav_trajectory_generation_cmake_amd import _native as nat
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    src = open(nat.HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"\b(mtg_[a-z0-9_]+)\s*\(", src))
+
+
+def _header_defines():
+    out = {}
+    for m in re.finditer(r"#define\s+(MTG_[A-Z0-9_]+)\s+\(?(-?\d+)u?\)?", open(nat.HEADER).read()):
+        out[m.group(1)] = int(m.group(2))
+    return out
+
+
+def test_header_and_binding_agree():
+    assert _header_functions() == set(nat.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = nat.load()
+    for name in _header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", nat.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln and ln.split()[-1].startswith("mtg_")}
+    assert exported == _header_functions()
+
+
+def test_constants_match_header():
+    for name, val in _header_defines().items():
+        if name in ("MTG_H_",):
+            continue
+        if hasattr(nat, name):
+            assert getattr(nat, name) == val, name
+    assert nat.load().mtg_abi_version() == _header_defines()["MTG_ABI_VERSION"]
+
+
+def test_status_strings():
+    for code in (0, -1, -2, -3, -4, -5, -6, -7, -8):
+        assert nat.status_string(code)
+    assert nat.status_string(-99)
+
+
+def test_one_hip_runtime_in_process():
+    """libmtg must bind to the same libamdhip64 as torch (see _native._share_torch_runtime)."""
+    pytest.importorskip("torch")
+    nat.load()
+    assert len(nat.hip_runtimes_mapped()) == 1, nat.hip_runtimes_mapped()
+
+
+def test_null_context_rejected():
+    lib = nat.load()
+    z = np.zeros(64)
+    m = np.zeros(64, np.uint8)
+    a = z.ctypes.data
+    assert lib.mtg_solve_linear_batch(None, 10, 3, 1, 4, 1, a, m.ctypes.data, a, a, None, None, None, None,
+                                      0) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_time_sweep_batch(None, 10, 3, 1, 4, 1, a, m.ctypes.data, a, 1, a, a, None,
+                                    0) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_set_stream(None, None) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_synchronize(None) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_enable_timing(None, 4) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_destroy(None) == nat.MTG_OK
+    assert lib.mtg_create(0, None) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_device_count(None) == nat.MTG_ERR_INVALID_ARGUMENT
+
+
+@pytest.mark.skipif(nat.device_count() > 0, reason="checks the no-device path")
+def test_no_device_fails_loudly():
+    from mav_trajectory_generation_cmake_amd import Context
+    with pytest.raises(nat.MTGError) as e:
+        Context(0)
+    assert e.value.code == nat.MTG_ERR_NO_DEVICE
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(nat.MTGError):
+        nat.load(str(tmp_path / "libmtg.so"))
+
+
+def test_host_generator_argument_errors():
+    lib = nat.load()
+    v = np.zeros(1000)
+    m = np.zeros(100, np.uint8)
+    t = np.zeros(100)
+    assert lib.mtg_host_random_vertices_path_batch(10, 3, 0, 5.0, 4, 0, 1, 2.0, 2.0, 6.5, v.ctypes.data,
+                                                   m.ctypes.data, t.ctypes.data, 1) != nat.MTG_OK
+    assert lib.mtg_host_random_vertices_path_batch(11, 3, 2, 5.0, 4, 0, 1, 2.0, 2.0, 6.5, v.ctypes.data,
+                                                   m.ctypes.data, t.ctypes.data, 1) != nat.MTG_OK
+
+
+def test_cpp_header_compiles_with_c_compiler(tmp_path):
+    """include/mtg.h is plain C: a C99 translation unit that includes it compiles and links."""
+    c = tmp_path / "t.c"
+    c.write_text('#include "mtg.h"\nint main(void){ return mtg_abi_version() == MTG_ABI_VERSION ? 0 : 1; }\n')
+    exe = tmp_path / "t"
+    libdir = os.path.dirname(nat.LIB_PATH)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                    str(exe), "-L", libdir, "-lmtg", "-Wl,-rpath," + libdir], check=True)
+    assert subprocess.run([str(exe)]).returncode == 0

@@ -1,0 +1,37 @@
+"""CPU checks on the gfx950 code the HIP sources compile to (hipcc cross-compiles without a GPU)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mav_trajectory_generation_cmake_amd", "csrc")
+
+hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+pytestmark = pytest.mark.skipif(not os.path.exists(hipcc), reason="hipcc not available")
+
+
+def _device_asm(src, tmp_path):
+    out = tmp_path / (os.path.basename(src) + ".s")
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    os.path.join(CSRC, src), "-o", str(out)], check=True, capture_output=True)
+    return out.read_text()
+
+
+def _kernel_bodies(asm, prefix):
+    bodies = {}
+    for m in re.finditer(r"^(%s\w*):" % prefix, asm, flags=re.M):
+        end = asm.find("s_endpgm", m.end())
+        bodies[m.group(1)] = asm[m.end():end]
+    return bodies
+
+
+def test_evaluate_range_has_no_fma(tmp_path):
+    """Polynomial::evaluate (polynomial.h:138-151) multiplies then adds; an FMA would change the
+    last bit and break bit-exact parity of evaluateRange with the reference."""
+    bodies = _kernel_bodies(_device_asm("mtg_eval.hip", tmp_path), r"_ZN3mtg17eval_range_kernel")
+    assert len(bodies) == 6  # N = 2, 4, ..., 12
+    for name, body in bodies.items():
+        assert not re.search(r"v_fma", body), name
