@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", action="store_true", help="two-kernel path (assembly + block Cholesky)")
+    ap.add_argument("--general-kernel", action="store_true",
+                    help="force the general LDS-resident fused kernel (A/B against the default)")
     args = ap.parse_args()
 
     import torch
@@ -123,7 +125,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     # one step = one launch of the solve on torch's current stream; the C ABI brackets every
     # launch with a HIP event pair on that same stream (ring of `steps` pairs)
-    step = ctx.solve_call(N, r, v_d, m_d, t_d, c_d, split=args.split)
+    step = ctx.solve_call(N, r, v_d, m_d, t_d, c_d, split=args.split, general=args.general_kernel)
     ctx.enable_timing(max(args.steps, 1))
 
     for _ in range(args.warmup):
@@ -156,7 +158,13 @@ def main():
     value = total / el
     bpt = algorithmic_bytes_per_traj(N, D, K)
     achieved = bpt * B / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profiles("solve_fused_kernel", B)
+    if args.split:
+        kname = "assemble+block_cholesky"
+    elif args.general_kernel or K > 12:
+        kname = "solve_fused_kernel"
+    else:
+        kname = "solve_reg_kernel"
+    traffic = traffic_from_profiles(kname, B)
     out = {
         "metric": "trajectories/sec (10-seg, N=10, 3-D min-snap) at 1/2/4/8 MI355X",
         "value": value,
@@ -174,11 +182,11 @@ def main():
         "config": {"workload": "config2: %d x (K=%d, N=%d, D=%d, r=SNAP) per GPU, device-resident" % (B, K, N, D),
                    "batch_per_gpu": B, "global_batch": B * world, "segments": K, "N": N, "D": D,
                    "derivative_to_optimize": r, "parallelism": "shard%d" % world,
-                   "kernel_path": "split" if args.split else "fused"},
+                   "kernel_path": kname},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
-                     "kernel": "solve_fused_kernel<10>" if not args.split else "assemble+block_cholesky",
+                     "kernel": kname,
                      "kernel_ms": kern_ms, "kernel_ms_min": float(np.min(per_launch)),
                      "kernel_ms_max": float(np.max(per_launch)), "gpu_ms_timed_region": gpu_ms,
                      "algorithmic_bytes_per_traj": bpt},

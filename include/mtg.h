@@ -69,6 +69,8 @@ extern "C" {
 #define MTG_FLAG_DEVICE_PTRS 1u        /* all array arguments are device pointers on the ctx device */
 #define MTG_FLAG_ASYNC 2u              /* do not synchronize the stream before returning */
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
+#define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
+                                          (default: the register-resident kernel when K <= 12) */
 
 typedef struct mtg_ctx mtg_ctx;
 

@@ -30,6 +30,7 @@ MTG_TRAJ_ERROR_MASK = 255
 MTG_FLAG_DEVICE_PTRS = 1
 MTG_FLAG_ASYNC = 2
 MTG_FLAG_SPLIT_KERNELS = 4
+MTG_FLAG_GENERAL_KERNEL = 8
 
 _c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
 

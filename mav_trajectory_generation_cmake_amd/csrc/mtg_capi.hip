@@ -189,7 +189,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, (flags & MTG_FLAG_GENERAL_KERNEL) != 0));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (!dev) {

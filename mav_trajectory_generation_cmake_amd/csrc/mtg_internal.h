@@ -27,8 +27,12 @@ struct SolveArgs {
 // when the per-trajectory working set cannot fit in LDS.
 bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes, int* traj_per_block);
 
-// Launch the fused solve kernel on `stream`.
-hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream);
+// Launch the fused solve on `stream`: the register-resident kernel (mtg_solve_reg.hip) when the
+// shape allows it (K <= 12, LDS slot fits) and `general` is false, else the general LDS-resident
+// kernel (mtg_kernels.hip).
+hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, bool general = false);
+bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);
+hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
 
 // Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
 // workspace, then the block-Cholesky solve + recovery.

@@ -37,128 +37,11 @@
 // free), and solves its own column.  G_v and z_v stay in LDS for the backward
 // sweep, which also recovers coefficients and the cost and streams them to HBM.
 // Everything is FP64 (the reference is FP64 throughout).
-#include "mtg_internal.h"
-#include "mtg.h"
-#include "mtg_tables.inc"
+#include "mtg_device.h"
 
-#include <float.h>
 #include <stdlib.h>
 
 namespace mtg {
-
-__constant__ double c_a1inv[MTG_A1INV_SIZE] = {MTG_A1INV_VALUES};
-__constant__ double c_htilde[MTG_HTILDE_SIZE] = {MTG_HTILDE_VALUES};
-
-// Block of 64 threads = one wave; all LDS traffic is intra-wave.
-constexpr int kBlock = 64;
-constexpr size_t kMaxLdsPerBlock = 64 * 1024;
-constexpr size_t kMaxLdsHard = 160 * 1024;
-
-// 1/x from v_rcp_f64 plus two Newton steps (full FP64 accuracy; no IEEE division sequence).
-__device__ __forceinline__ double rcp(double x) {
-#ifdef MTG_IEEE_DIV
-  return 1.0 / x;
-#endif
-  double y = __builtin_amdgcn_rcp(x);
-  double e = __builtin_fma(-x, y, 1.0);
-  y = __builtin_fma(y, e, y);
-  e = __builtin_fma(-x, y, 1.0);
-  return __builtin_fma(y, e, y);
-}
-
-// s[k] = T^k (k < H) and sc = T^(1-2R) = 1 / (T^R T^(R-1)): the time-scaling of one segment.
-template <int H, int R>
-__device__ __forceinline__ void seg_powers(double T, double (&s)[H], double& sc) {
-  static_assert(R >= 0 && R < H, "derivative_to_optimize must be in [0, N/2-1]");
-  s[0] = 1.0;
-#pragma unroll
-  for (int k = 1; k < H; ++k) s[k] = s[k - 1] * T;
-  if constexpr (R == 0) {
-    sc = T;
-  } else {
-    sc = rcp(s[R] * s[R - 1]);
-  }
-}
-
-__device__ __forceinline__ bool time_ok(double T) { return T >= DBL_EPSILON && T <= DBL_MAX; }
-
-template <int H>
-__device__ __forceinline__ void load_fixed(const double* vals, int v, int D, int d, unsigned m,
-                                           double (&x)[H]) {
-  const double* p = vals + ((size_t)v * H) * D + d;
-#pragma unroll
-  for (int k = 0; k < H; ++k) {
-    const double t = p[k * D];
-    x[k] = ((m >> k) & 1u) ? t : 0.0;
-  }
-}
-
-// S = L diag(d) L^T (L unit lower, below the diagonal of S; only the lower triangle of S is
-// read); dinv = 1/d.  Returns the smallest pivot (<= 0 or non-finite: R_pp is not SPD; the
-// reference never checks, lin_impl:355-368).
-template <int H>
-__device__ __forceinline__ double ldlt(double (&S)[H][H], double (&dinv)[H]) {
-  double pmin = DBL_MAX;
-  double dg[H];
-#pragma unroll
-  for (int j = 0; j < H; ++j) {
-    double w[H];
-    double dj = S[j][j];
-#pragma unroll
-    for (int k = 0; k < j; ++k) {
-      w[k] = S[j][k] * dg[k];
-      dj -= S[j][k] * w[k];
-    }
-    pmin = dj < pmin ? dj : pmin;
-    const double inv = rcp(dj);
-    dg[j] = dj;
-    dinv[j] = inv;
-#pragma unroll
-    for (int i = j + 1; i < H; ++i) {
-      double t = S[i][j];
-#pragma unroll
-      for (int k = 0; k < j; ++k) t -= S[i][k] * w[k];
-      S[i][j] = t * inv;
-    }
-  }
-  return pmin;
-}
-
-// x = S^-1 b with S factored in place by ldlt()
-template <int H>
-__device__ __forceinline__ void ldlt_solve(const double (&S)[H][H], const double (&dinv)[H],
-                                           const double (&b)[H], double (&x)[H]) {
-  double y[H];
-#pragma unroll
-  for (int i = 0; i < H; ++i) {
-    double t = b[i];
-#pragma unroll
-    for (int k = 0; k < i; ++k) t -= S[i][k] * y[k];
-    y[i] = t;
-  }
-#pragma unroll
-  for (int i = H - 1; i >= 0; --i) {
-    double t = y[i] * dinv[i];
-#pragma unroll
-    for (int k = i + 1; k < H; ++k) t -= S[k][i] * x[k];
-    x[i] = t;
-  }
-}
-
-// Per-trajectory LDS slot (doubles): exchange buffer (LG x h), G_v (K x h x h), Z_v (V x D x h:
-// z_v after the forward sweep, the pinned solution x_v after the backward sweep).
-__host__ __device__ __forceinline__ int slot_doubles(int H, int D, int K, int LG) {
-  return LG * H + K * H * H + (K + 1) * D * H;
-}
-
-// Re-materialise a uniform table pointer inside a loop so the compiler reloads the table
-// from the scalar cache instead of hoisting 100+ doubles into SGPRs and spilling them.
-typedef const __attribute__((address_space(4))) double cdouble;
-__device__ __forceinline__ cdouble* launder(const double* p) {
-  cdouble* q = (cdouble*)p;
-  asm volatile("" : "+s"(q));
-  return q;
-}
 
 template <int N, int R>
 __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg_log2) {
@@ -504,7 +387,10 @@ static hipError_t launch_fused_n(const SolveArgs& a, hipStream_t stream) {
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream) {
+hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, bool general) {
+  int lg;
+  size_t lds;
+  if (!general && reg_geometry(N, a.D, a.K, &lg, &lds)) return launch_solve_reg(N, a, stream);
   switch (N) {
     case 2: return launch_fused_n<2>(a, stream);
     case 4: return launch_fused_n<4>(a, stream);
