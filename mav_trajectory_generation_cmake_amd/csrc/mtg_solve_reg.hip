@@ -154,6 +154,271 @@ __device__ __forceinline__ void factor_solve(const double* xs, const double (&rh
   }
 }
 
+// Per-vertex scalars of the forward sweep (wave-uniform flags and this lane's segment scalings).
+template <int H>
+struct VertexIn {
+  bool has_prev, has_next;
+  unsigned mp, mc, mn;  // this trajectory's masks at v-1, v, v+1
+  unsigned xc1, xn1;    // fixed derivatives > 0 in any trajectory of the wave, at v and v+1
+  bool skip_bl0;        // BL column 0 multiplies zero in every lane
+  double xfp0;          // fixed position at v-1 (dimension lanes)
+  double scp, spc;      // segment v-1: T^(1-2r), T^c
+  double scn, snc;      // segment v:   T^(1-2r), T^c
+};
+
+// One forward block-Thomas step at vertex v (see solve_fused_kernel for the block equations):
+// assemble this lane's column of S_v (column lanes) or right-hand side (dimension lanes), exchange
+// the S columns through LDS, factor and solve.  PIN = derivatives pinned at v in every trajectory
+// of the wave: their rows are skipped at compile time.  Out: x = column c of G_v (column lanes) or
+// z_v (dimension lanes), 0 on pinned rows.
+template <int N, int R, unsigned PIN>
+__device__ __forceinline__ void vertex_solve(const VertexIn<N / 2>& in, bool is_g, bool is_d, int c, int cg,
+                                             const double (&gp)[N / 2], const double (&xfc)[N / 2],
+                                             const double (&xfn)[N / 2], const double (&sp)[N / 2],
+                                             const double (&sn)[N / 2], const double* rowBT, const double* rowTL,
+                                             cdouble* BLbase, cdouble* Hbase, double* xs, double (&x)[N / 2],
+                                             double& pmin) {
+  constexpr int H = N / 2;
+  constexpr int HP = even_up(H);
+  const bool c_free = is_g && !((in.mc >> cg) & 1u);
+  const bool c_free_n = is_g && in.has_next && !((in.mn >> cg) & 1u);
+
+  // per-lane inputs: a2 = -g_{v-1} (column lanes) or x^_{v-1} (dimension lanes);
+  // a1 = x_f,v and a3 = x_f,v+1 (dimension lanes; zero in column lanes)
+  double a2[H], a1b[H], a1t[H], a3[H];
+#pragma unroll
+  for (int k = 0; k < H; ++k) a2[k] = gp[k], a1b[k] = xfc[k], a1t[k] = xfc[k], a3[k] = xfn[k];
+  if (R >= 1) {  // translation-relative positions (solve_fused_kernel, DESIGN.md "Numerics")
+    const bool tp = in.has_prev && (in.mp & in.mc & 1u);
+    const bool tn = in.has_next && (in.mc & in.mn & 1u);
+    a1b[0] = tp ? xfc[0] - in.xfp0 : a1b[0];
+    a2[0] = tp ? 0.0 : a2[0];
+    a3[0] = tn ? xfn[0] - xfc[0] : a3[0];
+    a1t[0] = tn ? 0.0 : a1t[0];
+  }
+
+  double out[H], yy[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) out[i] = 0.0, yy[i] = 0.0;
+  if (in.has_prev) {  // bottom rows of H_{v-1}: BL a2 + BR a1
+    cdouble* BL = launder((const double*)BLbase);
+    double t[H];
+    // lane column of BR: column c (column lanes, if free at v) or 0 (dimension lanes, x_f,v[0])
+    const double kb = is_g ? (c_free ? in.spc : 0.0) : a1b[0];
+#pragma unroll
+    for (int i = 0; i < H; ++i)
+      if (!((PIN >> i) & 1u)) t[i] = rowBT[H + i] * kb;
+    if (!in.skip_bl0) {
+#pragma unroll
+      for (int i = 0; i < H; ++i)
+        if (!((PIN >> i) & 1u)) t[i] += BL[i * H] * a2[0];
+    }
+#pragma unroll
+    for (int j = 1; j < H; ++j) {
+      const double uj = sp[j] * a2[j];
+#pragma unroll
+      for (int i = 0; i < H; ++i)
+        if (!((PIN >> i) & 1u)) t[i] += BL[i * H + j] * uj;
+    }
+    if (in.xc1) {
+      cdouble* Hs = launder((const double*)Hbase);
+#pragma unroll
+      for (int j = 1; j < H; ++j) {
+        if (!((in.xc1 >> j) & 1u)) continue;
+        const double uj = sp[j] * a1b[j];
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+          if (!((PIN >> i) & 1u)) t[i] += Hs[(H + i) * N + H + j] * uj;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i)
+      if (!((PIN >> i) & 1u)) out[i] = (in.scp * sp[i]) * t[i];
+  }
+  if (in.has_next) {  // top rows of H_v: TL a1 + TR a3 (+ the G right-hand side: TR column c)
+    double t[H], y[H];
+    const double kt = is_g ? (c_free ? in.snc : 0.0) : a1t[0];
+    const double kyg = c_free_n ? in.snc : 0.0;  // column lanes: G right-hand side
+    const double kyd = is_g ? 0.0 : a3[0];       // dimension lanes: TR x_f,v+1[0]
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      if ((PIN >> i) & 1u) continue;
+      const double r = rowBT[i];
+      t[i] = rowTL[i] * kt + r * kyd;
+      y[i] = r * kyg;
+    }
+    if (in.xc1 | in.xn1) {
+      cdouble* Hs = launder((const double*)Hbase);
+#pragma unroll
+      for (int j = 1; j < H; ++j) {
+        if (!((in.xc1 >> j) & 1u)) continue;
+        const double wj = sn[j] * a1t[j];
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+          if (!((PIN >> i) & 1u)) t[i] += Hs[i * N + j] * wj;
+      }
+#pragma unroll
+      for (int j = 1; j < H; ++j) {
+        if (!((in.xn1 >> j) & 1u)) continue;
+        const double wj = sn[j] * a3[j];
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+          if (!((PIN >> i) & 1u)) t[i] += Hs[i * N + H + j] * wj;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+      if ((PIN >> i) & 1u) continue;
+      const double f = in.scn * sn[i];
+      out[i] += f * t[i];
+      yy[i] = f * y[i];
+    }
+  }
+
+  // column lanes: S column c (pinned rows 0; pinned column: e_c); all lanes: the right-hand side
+  // of their solve, G_v (column lanes: TR column c) or z_v (dimension lanes: -out), 0 on fixed rows
+  const double dflag = is_d ? 1.0 : 0.0;
+  double rhs[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    if ((PIN >> i) & 1u) {
+      rhs[i] = 0.0;
+      continue;
+    }
+    const double fm = ((in.mc >> i) & 1u) ? 0.0 : 1.0;
+    const double o = fm * out[i];
+    double sv = c_free ? o : (i == c ? 1.0 : 0.0);
+    asm volatile("" : "+v"(sv));
+    xs[c * HP + i] = sv;  // only column lanes' slots are read
+    rhs[i] = fm * yy[i] - dflag * o;
+  }
+  __syncthreads();
+  factor_solve<H, HP, PIN>(xs, rhs, x, pmin);
+  __syncthreads();
+}
+
+// Forward block-Thomas sweep over vertices 0..K, unrolled at compile time up to KMAX by template
+// recursion: step<V> returns early once V > K.  (A `for` loop with a `continue` guard unrolls too,
+// but makes every step a merge point of the whole loop-carried state, which the register allocator
+// pays for with ~70 register copies per vertex.)  G is statically indexed, so it stays in registers.
+template <int N, int R, int KMAX>
+struct Forward {
+  static constexpr int H = N / 2;
+  static constexpr unsigned HM = (1u << H) - 1u;
+  // context (per lane, constant over the sweep)
+  int K, D, d;
+  bool is_g, is_d;
+  int c, cg;
+  double gsign, tscale;
+  double* X;
+  double* xs;
+  const double* tms;
+  const uint8_t* msk;
+  const double* rowBT;
+  const double* rowTL;
+  cdouble* BLbase;
+  cdouble* Hbase;
+  // loop-carried state
+  int st = 0, n_free = 0;
+  double pmin = DBL_MAX;
+  uint32_t pin_cls = 0;  // per vertex, 2 bits: 0 none / 1 {position} / 2 all / 3 other, fixed in
+                         // every trajectory of the wave (wave-uniform)
+  double G[KMAX][H];     // column lanes: column c of G_v, v < K
+  double gp[H], xfc[H], xfn[H];
+  double sp[H], sn[H];
+  double scp = 0.0, scn = 0.0, spc = 0.0, snc = 0.0, xfp0 = 0.0;
+  unsigned mp = 0, mc = 0, mn = 0;
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int k = 0; k < H; ++k) gp[k] = 0.0, sp[k] = 0.0;
+    const double T0 = tms[0] * tscale;
+    if (!time_ok(T0)) st |= MTG_TRAJ_BAD_TIME;
+    seg_powers<H, R>(T0, sn, scn);
+    snc = lane_power<H>(sn, cg);
+    unsigned raw = msk[0];
+    if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
+    mc = raw & HM;
+    raw = msk[1];
+    if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
+    mn = raw & HM;
+    load_x<H>(X, 0, D, d, is_d ? mc : 0u, xfc);
+    load_x<H>(X, 1, D, d, is_d ? mn : 0u, xfn);
+  }
+
+  template <int V>
+  __device__ __forceinline__ void step() {
+    if constexpr (V <= KMAX) {
+      if (V > K) return;
+      const bool has_prev = V > 0, has_next = V < K;
+
+      // wave-uniform masks (scalar): identical masks in all lanes enable the skips below
+      const unsigned mm = mp | (mc << 8) | (mn << 16);
+      const unsigned u = __builtin_amdgcn_readfirstlane(mm);
+      const bool uni = __builtin_amdgcn_ballot_w64(mm != u) == 0;
+      const unsigned uc = (u >> 8) & HM, un = (u >> 16) & HM;
+      const unsigned pin = uni ? uc : 0u;
+      pin_cls |= (pin == 0u ? 0u : pin == 1u ? 1u : pin == HM ? 2u : 3u) << (2 * V);
+
+      double x[H];
+#pragma unroll
+      for (int i = 0; i < H; ++i) x[i] = 0.0;
+      // pin == HM: every derivative fixed at v in every trajectory, S_v = I and rhs = 0, so x = 0
+      if (pin != HM) {
+        // fixed derivatives other than the position, in any trajectory of the wave, at v / v+1:
+        // their columns of BR, TL, TR enter the dimension lanes' products through scalar loads
+        const unsigned xc1 = (uni ? uc : HM) & ~1u, xn1 = (uni ? un : HM) & ~1u;
+        // position fixed at v-1 and v in every trajectory: the BL column 0 term is zero in all lanes
+        const bool skip_bl0 = uni && R >= 1 && has_prev && ((u & uc) & 1u);
+        VertexIn<H> in{has_prev, has_next, mp, mc, mn, xc1, xn1, skip_bl0, xfp0, scp, spc, scn, snc};
+        if (pin == 1u)
+          vertex_solve<N, R, 1u>(in, is_g, is_d, c, cg, gp, xfc, xfn, sp, sn, rowBT, rowTL, BLbase, Hbase, xs, x,
+                                 pmin);
+        else
+          vertex_solve<N, R, 0u>(in, is_g, is_d, c, cg, gp, xfc, xfn, sp, sn, rowBT, rowTL, BLbase, Hbase, xs, x,
+                                 pmin);
+      }
+      if constexpr (V < KMAX) {
+        if (has_next) {
+#pragma unroll
+          for (int i = 0; i < H; ++i) G[V][i] = x[i];
+        }
+      }
+      if (is_d && pin != HM) {
+#pragma unroll
+        for (int i = 0; i < H; ++i)
+          if (!(((pin == 1u ? 1u : 0u) >> i) & 1u)) X[(V * H + i) * D + d] = xfc[i] + x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < H; ++i) gp[i] = __builtin_fma(gsign, x[i], xfc[i]);  // -g (xfc = 0) or x^
+      n_free += __builtin_popcount(~mc & HM);
+      if (!has_next) return;
+      xfp0 = xfc[0];
+      mp = mc;
+#pragma unroll
+      for (int k = 0; k < H; ++k) sp[k] = sn[k], xfc[k] = xfn[k];
+      scp = scn;
+      spc = snc;
+      mc = mn;
+      if (V + 1 < K) {
+        const double Tn = tms[V + 1] * tscale;
+        if (!time_ok(Tn)) st |= MTG_TRAJ_BAD_TIME;
+        seg_powers<H, R>(Tn, sn, scn);
+        snc = lane_power<H>(sn, cg);
+        const unsigned raw = msk[V + 2];
+        if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
+        mn = raw & HM;
+        load_x<H>(X, V + 2, D, d, is_d ? mn : 0u, xfn);
+      } else {
+        mn = 0;
+#pragma unroll
+        for (int k = 0; k < H; ++k) xfn[k] = 0.0;
+      }
+      step<V + 1>();
+    }
+  }
+};
+
 template <int N, int R, int KMAX>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void solve_reg_kernel(
     SolveArgs a, int lg_log2) {
@@ -179,6 +444,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const bool is_d = (c >= H) && (c < H + D);
   const int d = is_d ? c - H : 0;
   const int cg = is_g ? c : 0;
+  const double gsign = is_g ? -1.0 : 1.0;
 
   double* ht = lds;                                   // Htilde(N, R), row-major N x N
   double* xall = lds + N * N;                         // [tpb][V][H][D]
@@ -265,192 +531,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   const double* rowTL = ht + cg * N;        // [TL col | ...]
 
   // ---- forward sweep (see solve_fused_kernel for the block equations)
-  int st = 0, n_free = 0;
-  double pmin = DBL_MAX;
-  double G[KMAX][H];     // column lanes: column c of G_v, v < K
-  uint32_t pin_cls = 0;  // per vertex, 2 bits: 0 none / 1 {position} / 2 all / 3 other, fixed
-                         // in every trajectory of the wave (wave-uniform)
-  double gp[H], xfc[H], xfn[H];
-  double sp[H], sn[H], scp = 0.0, scn = 0.0, spc = 0.0, snc = 0.0;
-#pragma unroll
-  for (int k = 0; k < H; ++k) gp[k] = 0.0, sp[k] = 0.0;
-  {
-    const double T0 = tms[0] * tscale;
-    if (!time_ok(T0)) st |= MTG_TRAJ_BAD_TIME;
-    seg_powers<H, R>(T0, sn, scn);
-    snc = lane_power<H>(sn, cg);
-  }
-  unsigned raw = msk[0];
-  if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned mc = raw & HM;
-  raw = msk[1];
-  if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned mn = raw & HM;
-  unsigned mp = 0;
-  double xfp0 = 0.0;
-  load_x<H>(X, 0, D, d, is_d ? mc : 0u, xfc);
-  load_x<H>(X, 1, D, d, is_d ? mn : 0u, xfn);
-
-#pragma unroll
-  for (int v = 0; v <= KMAX; ++v) {
-    if (v > K) continue;  // (not break: a constant trip count lets the loop unroll fully)
-    const bool has_prev = v > 0, has_next = v < K;
-
-    // wave-uniform masks (scalar): identical masks in all lanes enable the skips below
-    const unsigned mm = mp | (mc << 8) | (mn << 16);
-    const unsigned u = __builtin_amdgcn_readfirstlane(mm);
-    const bool uni = __builtin_amdgcn_ballot_w64(mm != u) == 0;
-    const unsigned uc = (u >> 8) & HM, un = (u >> 16) & HM;
-    const unsigned pin = uni ? uc : 0u;
-    pin_cls |= (pin == 0u ? 0u : pin == 1u ? 1u : pin == HM ? 2u : 3u) << (2 * v);
-
-    double x[H];
-#pragma unroll
-    for (int i = 0; i < H; ++i) x[i] = 0.0;
-    // pin == HM: every derivative fixed at v in every trajectory, S_v = I and rhs = 0, so x = 0
-    if (pin != HM) {
-      // fixed derivatives other than the position, in any trajectory of the wave, at v / v+1:
-      // their columns of BR, TL, TR enter the dimension lanes' products through scalar loads
-      const unsigned xc1 = (uni ? uc : HM) & ~1u, xn1 = (uni ? un : HM) & ~1u;
-      const bool c_free = is_g && !((mc >> cg) & 1u);
-      const bool c_free_n = is_g && has_next && !((mn >> cg) & 1u);
-
-      // per-lane inputs: a2 = -g_{v-1} (column lanes) or x^_{v-1} (dimension lanes);
-      // a1 = x_f,v and a3 = x_f,v+1 (dimension lanes; zero in column lanes)
-      double a2[H], a1b[H], a1t[H], a3[H];
-#pragma unroll
-      for (int k = 0; k < H; ++k) a2[k] = gp[k], a1b[k] = xfc[k], a1t[k] = xfc[k], a3[k] = xfn[k];
-      if (R >= 1) {  // translation-relative positions (solve_fused_kernel, DESIGN.md "Numerics")
-        const bool tp = has_prev && (mp & mc & 1u);
-        const bool tn = has_next && (mc & mn & 1u);
-        a1b[0] = tp ? xfc[0] - xfp0 : a1b[0];
-        a2[0] = tp ? 0.0 : a2[0];
-        a3[0] = tn ? xfn[0] - xfc[0] : a3[0];
-        a1t[0] = tn ? 0.0 : a1t[0];
-      }
-
-      double out[H], yy[H];
-#pragma unroll
-      for (int i = 0; i < H; ++i) out[i] = 0.0, yy[i] = 0.0;
-      if (has_prev) {  // bottom rows of H_{v-1}: BL a2 + BR a1
-        cdouble* BL = launder((const double*)BLbase);
-        double t[H];
-        // lane column of BR: column c (column lanes, if free at v) or 0 (dimension lanes, x_f,v[0])
-        const double kb = is_g ? (c_free ? spc : 0.0) : a1b[0];
-#pragma unroll
-        for (int i = 0; i < H; ++i) t[i] = rowBT[H + i] * kb;
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          const double uj = (j == 0) ? a2[0] : sp[j] * a2[j];
-#pragma unroll
-          for (int i = 0; i < H; ++i) t[i] += BL[i * H + j] * uj;
-        }
-        if (xc1) {
-          cdouble* Hs = launder((const double*)Hbase);
-#pragma unroll
-          for (int j = 1; j < H; ++j) {
-            if (!((xc1 >> j) & 1u)) continue;
-            const double uj = sp[j] * a1b[j];
-#pragma unroll
-            for (int i = 0; i < H; ++i) t[i] += Hs[(H + i) * N + H + j] * uj;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < H; ++i) out[i] = (scp * sp[i]) * t[i];
-      }
-      if (has_next) {  // top rows of H_v: TL a1 + TR a3 (+ the G right-hand side: TR column c)
-        double t[H], y[H];
-        const double kt = is_g ? (c_free ? snc : 0.0) : a1t[0];
-        const double kyg = c_free_n ? snc : 0.0;  // column lanes: G right-hand side
-        const double kyd = is_g ? 0.0 : a3[0];    // dimension lanes: TR x_f,v+1[0]
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-          const double r = rowBT[i];
-          t[i] = rowTL[i] * kt + r * kyd;
-          y[i] = r * kyg;
-        }
-        if (xc1 | xn1) {
-          cdouble* Hs = launder((const double*)Hbase);
-#pragma unroll
-          for (int j = 1; j < H; ++j) {
-            if (!((xc1 >> j) & 1u)) continue;
-            const double wj = sn[j] * a1t[j];
-#pragma unroll
-            for (int i = 0; i < H; ++i) t[i] += Hs[i * N + j] * wj;
-          }
-#pragma unroll
-          for (int j = 1; j < H; ++j) {
-            if (!((xn1 >> j) & 1u)) continue;
-            const double wj = sn[j] * a3[j];
-#pragma unroll
-            for (int i = 0; i < H; ++i) t[i] += Hs[i * N + H + j] * wj;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-          const double f = scn * sn[i];
-          out[i] += f * t[i];
-          yy[i] = f * y[i];
-        }
-      }
-
-      // compile-time pinned pattern used by factor_solve: {position} (interior waypoints of every
-      // generator) or none (dense; other uniform patterns factor as per-lane identity rows)
-      const unsigned wpin = (pin == 1u) ? 1u : 0u;
-      double rhs[H];
-#pragma unroll
-      for (int i = 0; i < H; ++i) {
-        const bool fi = !((mc >> i) & 1u);
-        double sv = c_free ? (fi ? out[i] : 0.0) : (i == c ? 1.0 : 0.0);
-        double rg = fi ? yy[i] : 0.0;
-        double rd = fi ? -out[i] : 0.0;
-        asm volatile("" : "+v"(sv), "+v"(rg), "+v"(rd));  // branch-free selects
-        if (!((wpin >> i) & 1u)) xs[c * HP + i] = sv;    // only column lanes' slots are read
-        rhs[i] = is_g ? rg : rd;
-      }
-      __syncthreads();
-      if (wpin)
-        factor_solve<H, HP, 1u>(xs, rhs, x, pmin);
-      else
-        factor_solve<H, HP, 0u>(xs, rhs, x, pmin);
-      __syncthreads();
-    }
-    if (has_next) {
-#pragma unroll
-      for (int i = 0; i < H; ++i) G[v < KMAX ? v : 0][i] = x[i];
-    }
-    if (is_d && pin != HM) {
-#pragma unroll
-      for (int i = 0; i < H; ++i)
-        if (!(((pin == 1u ? 1u : 0u) >> i) & 1u)) X[(v * H + i) * D + d] = xfc[i] + x[i];
-    }
-#pragma unroll
-    for (int i = 0; i < H; ++i) gp[i] = is_g ? -x[i] : xfc[i] + x[i];
-    n_free += __builtin_popcount(~mc & HM);
-    if (has_next) {
-      xfp0 = xfc[0];
-      mp = mc;
-#pragma unroll
-      for (int k = 0; k < H; ++k) sp[k] = sn[k], xfc[k] = xfn[k];
-      scp = scn;
-      spc = snc;
-      mc = mn;
-      if (v + 1 < K) {
-        const double Tn = tms[v + 1] * tscale;
-        if (!time_ok(Tn)) st |= MTG_TRAJ_BAD_TIME;
-        seg_powers<H, R>(Tn, sn, scn);
-        snc = lane_power<H>(sn, cg);
-        raw = msk[v + 2];
-        if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
-        mn = raw & HM;
-        load_x<H>(X, v + 2, D, d, is_d ? mn : 0u, xfn);
-      } else {
-        mn = 0;
-#pragma unroll
-        for (int k = 0; k < H; ++k) xfn[k] = 0.0;
-      }
-    }
-  }
+  Forward<N, R, KMAX> fw{K, D, d, is_g, is_d, c, cg, gsign, tscale, X, xs, tms, msk, rowBT, rowTL, BLbase, Hbase};
+  fw.init();
+  fw.template step<0>();
+  int st = fw.st, n_free = fw.n_free;
+  const double pmin = fw.pmin;
+  const uint32_t pin_cls = fw.pin_cls;
+  double (&G)[KMAX][H] = fw.G;
+  double (&gp)[H] = fw.gp;
   if (!(pmin > 0.0 && pmin <= DBL_MAX)) st |= MTG_TRAJ_NOT_SPD;
   MTG_PHASE(2);
 
@@ -497,12 +585,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
   __syncthreads();
   MTG_PHASE(3);
 
-  // ---- epilogue: coefficients and cost per item (segment i, dimension dd), spread over the group
+  // ---- epilogue: coefficients and cost per item (segment i, dimension dd), spread over the group.
+  // c = diag(T^-j) A(1)^-1 S(T) [x_i - p 1; x_{i+1} - p 1] + p e_0 with p = x_i[0] (the polynomial of
+  // the translated end values is p(t) - p: only c_0 changes, and p_i no longer cancels against
+  // p_{i+1} in c_j, j >= h).  A(1)^-1 is diag(1/j!) on top and dense below; its dense rows (without
+  // column 0, which multiplies the translated zero) are read into registers once for all items:
+  // the G registers are dead here.
+  double A1b[H][N - 1];
+  double A1d[H];
+  {
+    const double* Ai1 = c_a1inv + MTG_A1INV_OFF(N);
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      double t = Ai1[j * N + j];
+      asm volatile("" : "+v"(t));
+      A1d[j] = t;
+#pragma unroll
+      for (int q = 1; q < N; ++q) {
+        double u = Ai1[(H + j) * N + q];
+        asm volatile("" : "+v"(u));
+        A1b[j][q - 1] = u;
+      }
+    }
+  }
   double cacc = 0.0;
+  int ii = c / D, dd = c - (c / D) * D;  // item it = ii * D + dd, advanced by LG per round
   for (int it = c; it < K * D; it += LG) {
-    const int i = it / D, dd = it - i * D;
-    cdouble* Hl = launder((const double*)Hbase);
-    cdouble* Ai1 = launder(c_a1inv + MTG_A1INV_OFF(N));
+    const int i = ii;
     const double T = tms[i] * tscale;
     double s[H], sc;
     seg_powers<H, R>(T, s, sc);
@@ -512,7 +621,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       sh[k] = s[k] * X[(i * H + k) * D + dd];
       sh[H + k] = s[k] * X[((i + 1) * H + k) * D + dd];
     }
-    const double p0 = sh[0];  // recover p(t) - p_i, then c_0 = p_i (solve_fused_kernel epilogue)
+    const double p0 = sh[0];
     sh[0] = 0.0;
     sh[H] -= p0;
     if (a.coeffs) {
@@ -523,11 +632,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       for (int j = 0; j < N; ++j) {
         double acc;
         if (j < H) {
-          acc = (j == 0) ? p0 : Ai1[j * N + j] * sh[j];
+          acc = (j == 0) ? p0 : A1d[j] * sh[j];
         } else {
           acc = 0.0;
 #pragma unroll
-          for (int q = 0; q < N; ++q) acc += Ai1[j * N + q] * sh[q];
+          for (int q = 1; q < N; ++q) acc += A1b[j - H][q - 1] * sh[q];
         }
         outc[j] = acc * tp;
         tp *= tinv;
@@ -538,7 +647,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(outc[2 * j], outc[2 * j + 1]);
       }
     }
-    if (a.cost_out) {
+    if (a.cost_out) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)
+      cdouble* Hl = launder((const double*)Hbase);
       if (R == 0) sh[0] = p0, sh[H] += p0;
       double q = 0.0;
 #pragma unroll
@@ -550,6 +660,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
       }
       cacc += sc * q;
     }
+    dd += LG;
+    while (dd >= D) dd -= D, ++ii;
   }
 #ifdef MTG_PHASE_TIMING
   MTG_PHASE(4);
