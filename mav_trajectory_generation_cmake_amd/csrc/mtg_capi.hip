@@ -325,7 +325,7 @@ int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_op
   std::lock_guard<std::mutex> g(ctx->mu);
   return run_solve(ctx, N, D, K, derivative_to_optimize, batch, values, fixed_mask, times, nullptr,
                    nullptr, nullptr, cost_out, status, n_candidates, scales,
-                   flags & ~MTG_FLAG_SPLIT_KERNELS);
+                   flags);
 }
 
 int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,

@@ -148,18 +148,4 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   return hipGetLastError();
 }
 
-// Two-kernel path: not yet built in this revision.
-size_t split_workspace_bytes(int N, int D, int K, int64_t B) {
-  const int H = N / 2;
-  return sizeof(double) * (size_t)B * (K + 1) * H * (2 * H + D);
-}
-
-hipError_t launch_solve_split(int N, const SolveArgs& a, void* workspace, hipStream_t stream) {
-  (void)N;
-  (void)a;
-  (void)workspace;
-  (void)stream;
-  return hipErrorNotSupported;
-}
-
 }  // namespace mtg

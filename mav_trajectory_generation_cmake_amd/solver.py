@@ -157,7 +157,7 @@ class Context:
         return out
 
     def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
-                         asynchronous=False):
+                         asynchronous=False, split=False):
         dev = _is_torch(values) and values.is_cuda
         B, V, h, D = values.shape
         K = V - 1
@@ -175,6 +175,8 @@ class Context:
             cost = cost if cost is not None else np.empty((B, C))
             flags = 0
             self.reset_stream()
+        if split:
+            flags |= nat.MTG_FLAG_SPLIT_KERNELS
         rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                             _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
         nat.check(rc, self.handle)

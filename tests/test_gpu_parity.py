@@ -17,18 +17,24 @@ pytestmark = pytest.mark.gpu
 TRUTH_TOL = 1e-9
 ORACLE_TOL_N10 = 1e-6
 
+# the three solve paths behind mtg_solve_linear_batch: the default (register-resident kernel for
+# K <= 12, else the general one), the general LDS-resident fused kernel, and the two-kernel split path
+PATHS = {"default": {}, "general": {"general": True}, "split": {"split": True}}
+
 
 def _oracle():
     from oracle import pyoracle
     return pyoracle
 
 
+@pytest.mark.parametrize("path", sorted(PATHS))
 @pytest.mark.parametrize("case", golden_cases())
-def test_golden_truth(gpu_ctx, case):
+def test_golden_truth(gpu_ctx, case, path):
     g = load_golden(case)
     N, r = int(g["N"]), int(g["r"])
     vals, mask = to_abi(g["values"], g["mask"], N)
-    out = gpu_ctx.solve_linear_batch(N, r, vals, mask, g["times"], free=True, n_free=True, cost=True, status=True)
+    out = gpu_ctx.solve_linear_batch(N, r, vals, mask, g["times"], free=True, n_free=True, cost=True, status=True,
+                                     **PATHS[path])
     assert np.all(out["status"] & 0xFF == 0), out["status"]
     err = scale_normalised_error(out["coeffs"], g["coeffs"], g["times"])
     assert err <= TRUTH_TOL, (case, err)
@@ -65,12 +71,13 @@ def _bench_batch(B, seed0=0, K=10, N=10):
     return random_vertices_path_batch(N, 3, K, B, seed0=seed0)
 
 
-def test_vs_oracle_bench_generator(gpu_ctx):
+@pytest.mark.parametrize("path", sorted(PATHS))
+def test_vs_oracle_bench_generator(gpu_ctx, path):
     """Config 2 shape: bench generator, N=10, K=10, D=3, SNAP; GPU vs the FP64 oracle."""
     O = _oracle()
     B = 256
     vals, mask, times = _bench_batch(B, seed0=1000)
-    out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, cost=True, status=True)
+    out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, cost=True, status=True, **PATHS[path])
     assert np.all(out["status"] == 0)
     ref, cost = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times, want_cost=True)
     err = scale_normalised_error(out["coeffs"], ref, times)
@@ -166,25 +173,50 @@ def test_free_values_ignored(gpu_ctx):
     np.testing.assert_array_equal(a["coeffs"], b["coeffs"])
 
 
-@pytest.mark.parametrize("K", [1, 2, 50, 100])
-def test_segment_counts_vs_oracle(gpu_ctx, K):
-    """The reference bench's K in {2, 10, 50, 100} (src/polynomial_timing_evaluation.cpp:117) plus K=1."""
+@pytest.mark.parametrize("path", sorted(PATHS))
+@pytest.mark.parametrize("K", [1, 2, 3, 5, 9, 12, 13, 50, 100])
+def test_segment_counts_vs_oracle(gpu_ctx, K, path):
+    """The reference bench's K in {2, 10, 50, 100} (src/polynomial_timing_evaluation.cpp:117), K=1, and
+    the register kernel's compile-time bounds (KMAX 4 / 8 / 10 / 12; 13 falls back to the general one)."""
     O = _oracle()
     B = 8
     vals, mask, times = _bench_batch(B, seed0=77, K=K)
-    out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True)
+    out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True, **PATHS[path])
     assert np.all(out["status"] == 0)
     ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
     assert scale_normalised_error(out["coeffs"], ref, times) <= 1e-6
     assert check_path(vals, mask, times, out["coeffs"], 10, relative=True) < 1e-8
 
 
-def test_time_sweep_matches_solves(gpu_ctx):
+def test_paths_agree_mixed_masks(gpu_ctx):
+    """Per-trajectory masks that differ inside a wave (dense fallback of the register kernel) and
+    unaligned batch sizes: all three paths agree with each other and with the oracle."""
+    O = _oracle()
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch
+    B = 203
+    vals, mask, times = random_vertices_batch(10, 3, 7, B, [-10, -20, -10], [10, 20, 10], seed0=9, max_derivative=4)
+    rng = np.random.default_rng(5)
+    mask = mask.copy()
+    # interior vertices: random extra fixed derivatives per trajectory
+    extra = rng.integers(0, 32, size=mask[:, 1:-1].shape).astype(np.uint8) & rng.integers(0, 2, size=mask[:, 1:-1].shape).astype(np.uint8) * 0x1E
+    mask[:, 1:-1] |= extra
+    ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
+    outs = {p: gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True, cost=True, **PATHS[p])
+            for p in PATHS}
+    for p, o in outs.items():
+        assert np.all(o["status"] == 0), p
+        assert scale_normalised_error(o["coeffs"], ref, times) <= 1e-6, p
+    for p in ("general", "split"):
+        assert scale_normalised_error(outs[p]["coeffs"], outs["default"]["coeffs"], times) <= 1e-9, p
+
+
+@pytest.mark.parametrize("path", ["default", "split"])
+def test_time_sweep_matches_solves(gpu_ctx, path):
     """mtg_time_sweep_batch == computeCost of separate solves at scaled times."""
     B = 64
     vals, mask, times = _bench_batch(B, seed0=3)
     scales = 0.5 + np.arange(64) / 63.0
-    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales)
+    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, split=(path == "split"))
     for ci in (0, 17, 63):
         ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times * scales[ci], cost=True)["cost"]
         np.testing.assert_allclose(J[:, ci], ref, rtol=1e-12, atol=0)
