@@ -18,7 +18,7 @@
 
 namespace mtg {
 
-namespace {
+namespace split {
 
 __host__ __device__ constexpr int tri(int h) { return h * (h + 1) / 2; }
 __host__ __device__ inline int ws_elems(int H, int D) { return tri(H) + H * H + H * D; }
@@ -325,14 +325,15 @@ hipError_t launch_split_n(const SolveArgs& a, double* ws, hipStream_t stream) {
   return hipErrorInvalidValue;
 }
 
-}  // namespace
+}  // namespace split
 
 size_t split_workspace_bytes(int N, int D, int K, int64_t B) {
   const int H = N / 2;
-  return sizeof(double) * (size_t)(K + 1) * ws_elems(H, D) * (size_t)B;
+  return sizeof(double) * (size_t)(K + 1) * split::ws_elems(H, D) * (size_t)B;
 }
 
 hipError_t launch_solve_split(int N, const SolveArgs& a, void* workspace, hipStream_t stream) {
+  using namespace split;
   double* ws = static_cast<double*>(workspace);
   switch (N) {
     case 2: return launch_split_n<2>(a, ws, stream);

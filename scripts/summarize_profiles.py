@@ -12,7 +12,7 @@ gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md "HBM [CDNA4]" (FETCH_SIZE = 
 with 128-B requests).  Infinity-Cache (L3) hits are counted by these counters, so at sizes whose
 inputs stay L3-resident between launches this over-states true HBM bytes.
 
-usage: summarize_profiles.py TAG B [B ...]
+usage: summarize_profiles.py TAG B [B ...]      (reads gpurun_out/prof<SRC>_b<B>, SRC from $PROF_SRC)
 """
 import csv
 import json
@@ -55,7 +55,7 @@ def main():
     tpath = os.path.join(prof, "pmc_traffic.json")
     traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
     for B in batches:
-        src = os.path.join(ROOT, "gpurun_out", "prof_b%s" % B)
+        src = os.path.join(ROOT, "gpurun_out", "prof%s_b%s" % (os.environ.get("PROF_SRC", ""), B))
         stats = os.path.join(src, "trace", "run_kernel_stats.csv")
         shutil.copy(stats, os.path.join(prof, "%s_b%s_kernel_stats.csv" % (tag, B)))
         pmc = {}
