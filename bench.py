@@ -1,13 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark: trajectories/s of the batched 10-segment N=10 3-D minimum-snap solve.
 
-Workload (BASELINE.json configs[1], "config 2"): per GPU a batch of B = 1e4
+Default workload (BASELINE.json configs[1], "config 2"): per GPU a batch of B = 1e4
 trajectories from the reference bench generator
 createRandomVerticesPath(3, 10, 5.0, SNAP, seed) + estimateSegmentTimes(2, 2, 6.5)
 (src/polynomial_timing_evaluation.cpp:34-112), seeds rank*B .. rank*B+B-1 (so
 at N = 8 with --batch 125000 this is exactly config 3's 1e6 sharded batch).
 One step = one batched setupFromVertices + solveLinear of the whole batch
 (fused HIP kernel, inputs already resident in HBM, coefficients written to HBM).
+
+Other workloads (--workload), each its own JSON line:
+  config4  N=12, K=20, r=JERK: createRandomVertices(SNAP, 20, [-10,-20,-10], [10,20,10], seed)
+           + estimateSegmentTimes(3, 5) (src/vertex.cpp:27-79, :162-178)
+  config5  the config-2 problems, solved once (untimed), then one step = the cost of the solved
+           derivatives at 64 candidate time allocations (getCostAndGradientDerivative at
+           T_c = s_c T, s_c = 0.5 + c/63; mtg_cost_at_times_batch)
 
 Multi-GPU: one process per GPU (torchrun), contiguous shards, no data-path
 collective ("scaling": "weak"); a barrier + MAX-over-ranks of the timed region.
@@ -28,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+C5_CANDIDATES = 64
 
 
 def algorithmic_bytes_per_traj(N, D, K):
@@ -37,18 +45,10 @@ def algorithmic_bytes_per_traj(N, D, K):
     return V * h * D * 8 + V + K * 8 + K * D * N * 8
 
 
-def traffic_from_profiles(kernel_prefix, batch):
-    """HBM bytes per launch of the solve kernel from the committed PMC summary (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        ent = d.get(kernel_prefix, {}).get(str(batch))
-        return None if ent is None else float(ent["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+def cost_sweep_bytes_per_traj(N, D, K, C):
+    """mtg_cost_at_times_batch: vertex derivatives [V][h][D] + times [K] in, costs [C] out."""
+    V, h = K + 1, N // 2
+    return V * h * D * 8 + K * 8 + C * 8
 
 
 def shard_seed0(rank, batch_per_rank):
@@ -67,12 +67,31 @@ def max_over_ranks(x, dist, device):
     return float(t.item())
 
 
-def cpu_baseline(values, mask, times, N, r, target_s, threads):
-    """Oracle (faithful C restatement of lin_impl, dense QR in place of SparseQR) on host cores."""
+def traffic_from_profiles(kernel_prefix, batch):
+    """HBM bytes per launch of the solve kernel from the committed PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        ent = d.get(kernel_prefix, {}).get(str(batch))
+        return None if ent is None else float(ent["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def _oracle_lib():
     from oracle import pyoracle
     lib = pyoracle.build(build_dir="_build_bench", arch=os.environ.get("MTG_ORACLE_ARCH", "native"))
     pyoracle._LIB = None
     pyoracle.lib(lib)  # the copy built on this host with -march=native
+    return pyoracle
+
+
+def cpu_baseline(values, mask, times, N, r, target_s, threads):
+    """Oracle (faithful C restatement of lin_impl, dense QR in place of SparseQR) on host cores."""
+    pyoracle = _oracle_lib()
     m32 = mask.astype(np.uint32)
     done = 0
     t0 = time.perf_counter()
@@ -85,14 +104,38 @@ def cpu_baseline(values, mask, times, N, r, target_s, threads):
     return done / el, el, done
 
 
+def cpu_baseline_cost(xfull, times, scales, N, r, target_s, threads):
+    """Oracle getCostAndGradientDerivative at candidate times: per candidate the reference's
+    updateSegmentTimes (A, Schur A^-1, Q) and d^T R d."""
+    pyoracle = _oracle_lib()
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        pyoracle.cost_at_times_batch(N, r, xfull, times, scales, threads=threads)
+        done += len(xfull) * len(scales)
+        el = time.perf_counter() - t0
+        if el >= target_s:
+            break
+    return done / el, el, done
+
+
+def make_problems(workload, N, K, B, seed0):
+    import mav_trajectory_generation_cmake_amd as mtg
+    if workload == "config4":
+        return mtg.random_vertices_batch(N, 3, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=seed0,
+                                         max_derivative=4, v_max=3.0, a_max=5.0)
+    return mtg.random_vertices_path_batch(N, 3, K, B, seed0=seed0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (config 2: 1e4)")
-    ap.add_argument("--segments", type=int, default=10)
-    ap.add_argument("--N", type=int, default=10)
+    ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2")
+    ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (configs 2, 4, 5: 1e4)")
+    ap.add_argument("--segments", type=int, default=None)
+    ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -114,18 +157,40 @@ def main():
 
     import mav_trajectory_generation_cmake_amd as mtg
 
-    N, K, D, r = args.N, args.segments, 3, 4
+    wl = args.workload
+    if wl == "config4":
+        N, K, r = args.N or 12, args.segments or 20, 3
+    else:
+        N, K, r = args.N or 10, args.segments or 10, 4
+    D = 3
     B = args.batch
-    values, mask, times = mtg.random_vertices_path_batch(N, D, K, B, seed0=shard_seed0(rank, B))
+    values, mask, times = make_problems(wl, N, K, B, shard_seed0(rank, B))
     v_d = torch.from_numpy(values).to(dev)
     m_d = torch.from_numpy(mask).to(dev)
     t_d = torch.from_numpy(times).to(dev)
-    c_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
     ctx = mtg.Context(local)
     stream = torch.cuda.current_stream(dev)
-    # one step = one launch of the solve on torch's current stream; the C ABI brackets every
-    # launch with a HIP event pair on that same stream (ring of `steps` pairs)
-    step = ctx.solve_call(N, r, v_d, m_d, t_d, c_d, split=args.split, general=args.general_kernel)
+    if wl == "config5":
+        # solve once (untimed) for the free derivatives, then time the candidate-cost sweep
+        sol = ctx.solve_linear_batch(N, r, values, mask, times, free=True)
+        xfull = mtg.full_vertex_values(values, mask, sol["free"], N)
+        scales = np.repeat((0.5 + np.arange(C5_CANDIDATES) / (C5_CANDIDATES - 1.0))[:, None], K, axis=1)
+        x_d = torch.from_numpy(xfull).to(dev)
+        s_d = torch.from_numpy(np.ascontiguousarray(scales)).to(dev)
+        out_d = torch.empty((B, C5_CANDIDATES), dtype=torch.float64, device=dev)
+        step = ctx.cost_call(N, r, x_d, t_d, s_d, out_d)
+        kname = "cost_at_times_kernel"
+    else:
+        out_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
+        # one step = one launch of the solve on torch's current stream; the C ABI brackets every
+        # launch with a HIP event pair on that same stream (ring of `steps` pairs)
+        step = ctx.solve_call(N, r, v_d, m_d, t_d, out_d, split=args.split, general=args.general_kernel)
+        if args.split:
+            kname = "assemble+block_cholesky"
+        elif args.general_kernel or K > 12 or (N == 12 and K > 8):
+            kname = "solve_fused_kernel"
+        else:
+            kname = "solve_reg_kernel"
     ctx.enable_timing(max(args.steps, 1))
 
     for _ in range(args.warmup):
@@ -150,25 +215,39 @@ def main():
     gpu_ms = g0.elapsed_time(g1)
     el = max_over_ranks(el, dist if world > 1 else None, dev)
 
-    # spot check of the timed outputs (finite, constraint continuity) -- not timed
-    c = c_d.cpu().numpy()
-    assert np.isfinite(c).all(), "non-finite coefficients"
+    # spot check of the timed outputs (finite) -- not timed
+    assert np.isfinite(out_d.cpu().numpy()).all(), "non-finite outputs"
 
-    total = B * world * args.steps
-    value = total / el
-    bpt = algorithmic_bytes_per_traj(N, D, K)
-    achieved = bpt * B / (kern_ms * 1e-3) / 1e9
-    if args.split:
-        kname = "assemble+block_cholesky"
-    elif args.general_kernel or K > 12:
-        kname = "solve_fused_kernel"
+    if wl == "config5":
+        units = B * C5_CANDIDATES
+        bpt = cost_sweep_bytes_per_traj(N, D, K, C5_CANDIDATES)
+        metric = "trajectory-candidate costs/sec (config 5: 64 time allocations x 10-seg N=10 3-D)"
+        unit = "candidate costs/s"
+        workload = "config5: %d x 64 candidate allocations (K=%d, N=%d, D=%d, r=SNAP) per GPU, d fixed" % (B, K, N, D)
+        data = ("synthetic: config-2 problems (createRandomVerticesPath + estimateSegmentTimes(2,2,6.5)) solved once; "
+                "candidates T_c = (0.5 + c/63) T")
     else:
-        kname = "solve_reg_kernel"
+        units = B
+        bpt = algorithmic_bytes_per_traj(N, D, K)
+        if wl == "config4":
+            metric = "trajectories/sec (config 4: 20-seg, N=12, 3-D min-jerk)"
+            workload = "config4: %d x (K=%d, N=%d, D=%d, r=JERK) per GPU, device-resident" % (B, K, N, D)
+            data = ("synthetic: createRandomVertices(SNAP,20,[-10,-20,-10],[10,20,10],seed) "
+                    "+ estimateSegmentTimes(3,5), seeds rank*B..rank*B+B-1")
+        else:
+            metric = "trajectories/sec (10-seg, N=10, 3-D min-snap) at 1/2/4/8 MI355X"
+            workload = "config2: %d x (K=%d, N=%d, D=%d, r=SNAP) per GPU, device-resident" % (B, K, N, D)
+            data = ("synthetic: reference bench generator createRandomVerticesPath(3,10,5.0,SNAP,seed) "
+                    "+ estimateSegmentTimes(2,2,6.5), seeds rank*B..rank*B+B-1")
+        unit = "trajectories/s"
+    total = units * world * args.steps
+    value = total / el
+    achieved = bpt * B / (kern_ms * 1e-3) / 1e9
     traffic = traffic_from_profiles(kname, B)
     out = {
-        "metric": "trajectories/sec (10-seg, N=10, 3-D min-snap) at 1/2/4/8 MI355X",
+        "metric": metric,
         "value": value,
-        "unit": "trajectories/s",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -177,12 +256,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: reference bench generator createRandomVerticesPath(3,10,5.0,SNAP,seed) "
-                "+ estimateSegmentTimes(2,2,6.5), seeds rank*B..rank*B+B-1",
-        "config": {"workload": "config2: %d x (K=%d, N=%d, D=%d, r=SNAP) per GPU, device-resident" % (B, K, N, D),
-                   "batch_per_gpu": B, "global_batch": B * world, "segments": K, "N": N, "D": D,
-                   "derivative_to_optimize": r, "parallelism": "shard%d" % world,
-                   "kernel_path": kname},
+        "data": data,
+        "config": {"workload": workload, "batch_per_gpu": B, "global_batch": B * world, "segments": K, "N": N,
+                   "D": D, "derivative_to_optimize": r, "parallelism": "shard%d" % world, "kernel_path": kname},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
@@ -195,11 +271,17 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:
         threads = int(os.environ.get("MTG_CPU_THREADS", min(16, os.cpu_count() or 1)))
         S = min(args.cpu_sample, B)
-        rate, cel, done = cpu_baseline(values[:S], mask[:S], times[:S], N, r, args.cpu_seconds, threads)
-        out["cpu_baseline"] = {"value": rate, "unit": "trajectories/s", "cores": threads, "kind": "port",
-                               "sample": "%d trajectories of this rank's shard, solved repeatedly for %.1f s "
-                                         "(%d solves) by the oracle restatement (-O3 -march=native, OpenMP)"
-                                         % (S, cel, done)}
+        if wl == "config5":
+            S = min(S, 2000)
+            rate, cel, done = cpu_baseline_cost(xfull[:S], times[:S], scales, N, r, args.cpu_seconds, threads)
+            sample = ("%d trajectories x %d candidates of this rank's shard, evaluated repeatedly for %.1f s "
+                      "(%d candidate costs) by the oracle restatement (-O3 -march=native, OpenMP)"
+                      % (S, C5_CANDIDATES, cel, done))
+        else:
+            rate, cel, done = cpu_baseline(values[:S], mask[:S], times[:S], N, r, args.cpu_seconds, threads)
+            sample = ("%d trajectories of this rank's shard, solved repeatedly for %.1f s "
+                      "(%d solves) by the oracle restatement (-O3 -march=native, OpenMP)" % (S, cel, done))
+        out["cpu_baseline"] = {"value": rate, "unit": unit, "cores": threads, "kind": "port", "sample": sample}
     ctx.close()
     if rank == 0:
         print(json.dumps(out))

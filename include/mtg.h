@@ -133,6 +133,20 @@ int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_op
                          const double* times, int n_candidates, const double* scales,
                          double* cost_out, int32_t* status, unsigned flags);
 
+/* Cost (and gradient) of FIXED vertex derivatives at candidate segment times: the reference's
+ * getCostAndGradientDerivative (polynomial_optimization_nonlinear_impl.h:1452-1520) evaluated at
+ * perturbed times, as its numerical time gradient does (getCostAndGradientTime :2153-2238):
+ *   J(b, c) = sum_dims d^T R(T_c) d   (no 1/2, unlike computeCost)
+ *   grad(b, c, dim) = 2 (R(T_c) d)_free   (free derivatives in the reference (vertex, derivative)
+ *                                          order; only with fixed_mask, entries >= n_free left 0)
+ * with T_c[i] = times[b][i] * scales[c][i].  vertex_values [B][V][h][D] holds ALL derivatives of
+ * every vertex (fixed values and the solved free ones, e.g. from free_out); fixed_mask [B][V] is
+ * needed only for the gradient.  cost_out [B][C]; grad_out [B][C][D][V*h] (nullable). */
+int mtg_cost_at_times_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                            int64_t batch, const double* vertex_values, const uint8_t* fixed_mask,
+                            const double* times, int n_candidates, const double* scales,
+                            double* cost_out, double* grad_out, unsigned flags);
+
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);

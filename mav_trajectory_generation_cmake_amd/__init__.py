@@ -8,8 +8,9 @@ host layer over that ABI.  See DESIGN.md.
 """
 from . import _native
 from ._native import MTGError, device_count, load
-from .solver import (Context, default_context, random_vertices_batch, random_vertices_path_batch,
-                     solve_linear_batch)
+from .solver import (Context, default_context, full_vertex_values, random_vertices_batch,
+                     random_vertices_path_batch, solve_linear_batch)
 
-__all__ = ["MTGError", "Context", "default_context", "device_count", "load", "random_vertices_batch",
+__all__ = ["MTGError", "Context", "default_context", "device_count", "full_vertex_values", "load",
+           "random_vertices_batch",
            "random_vertices_path_batch", "solve_linear_batch", "_native"]

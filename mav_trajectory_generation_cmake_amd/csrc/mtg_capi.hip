@@ -328,6 +328,69 @@ int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_op
                    flags);
 }
 
+int mtg_cost_at_times_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                            int64_t batch, const double* vertex_values, const uint8_t* fixed_mask,
+                            const double* times, int n_candidates, const double* scales,
+                            double* cost_out, double* grad_out, unsigned flags) {
+  int rc = check_shape(ctx, N, D, K, derivative_to_optimize, batch);
+  if (rc != MTG_OK) return rc;
+  if (n_candidates < 1) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "n_candidates must be >= 1");
+  if (batch == 0) return MTG_OK;
+  if (!vertex_values || !times || !scales || !cost_out || (grad_out && !fixed_mask))
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT,
+                     "vertex_values, times, scales, cost_out are required; grad_out needs fixed_mask");
+  if (mtg::cost_lds_bytes(N, D, K) > 64 * 1024)
+    return set_error(ctx, MTG_ERR_TOO_LARGE, "per-trajectory cost tables exceed LDS (reduce K or D)");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int V = K + 1, h = N / 2, C = n_candidates;
+  const size_t b_vals = sizeof(double) * (size_t)batch * V * h * D, b_mask = grad_out ? (size_t)batch * V : 0,
+               b_times = sizeof(double) * (size_t)batch * K, b_scales = sizeof(double) * (size_t)C * K,
+               b_cost = sizeof(double) * (size_t)batch * C,
+               b_grad = grad_out ? sizeof(double) * (size_t)batch * C * D * V * h : 0;
+  const double* d_vals = vertex_values;
+  const uint8_t* d_mask = fixed_mask;
+  const double *d_times = times, *d_scales = scales;
+  double *d_cost = cost_out, *d_grad = grad_out;
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  char* base = nullptr;
+  size_t o_cost = 0, o_grad = 0;
+  if (!dev) {
+    size_t off = 0;
+    const size_t o_vals = off; off = align_up(off + b_vals);
+    const size_t o_mask = off; off = align_up(off + b_mask);
+    const size_t o_times = off; off = align_up(off + b_times);
+    const size_t o_scales = off; off = align_up(off + b_scales);
+    o_cost = off; off = align_up(off + b_cost);
+    o_grad = off; off = align_up(off + b_grad);
+    MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+    base = static_cast<char*>(ctx->staging);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_vals, vertex_values, b_vals, hipMemcpyHostToDevice, ctx->stream));
+    if (b_mask) MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_mask, fixed_mask, b_mask, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_scales, scales, b_scales, hipMemcpyHostToDevice, ctx->stream));
+    d_vals = reinterpret_cast<const double*>(base + o_vals);
+    d_mask = b_mask ? reinterpret_cast<const uint8_t*>(base + o_mask) : nullptr;
+    d_times = reinterpret_cast<const double*>(base + o_times);
+    d_scales = reinterpret_cast<const double*>(base + o_scales);
+    d_cost = reinterpret_cast<double*>(base + o_cost);
+    d_grad = grad_out ? reinterpret_cast<double*>(base + o_grad) : nullptr;
+  }
+  if (d_grad) MTG_HIP_TRY(ctx, hipMemsetAsync(d_grad, 0, b_grad, ctx->stream));
+  MTG_HIP_TRY(ctx, time_begin(ctx));
+  MTG_HIP_TRY(ctx, mtg::launch_cost_at_times(N, derivative_to_optimize, d_vals, d_mask, d_times, d_scales, d_cost,
+                                             d_grad, batch, K, D, C, ctx->stream));
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  if (!dev) {
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(cost_out, base + o_cost, b_cost, hipMemcpyDeviceToHost, ctx->stream));
+    if (grad_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(grad_out, base + o_grad, b_grad, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  } else if (!(flags & MTG_FLAG_ASYNC)) {
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return MTG_OK;
+}
+
 int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
                              const double* coeffs, const double* times, double t_start,
                              double t_end, double dt, int derivative, int64_t* counts,

@@ -39,6 +39,12 @@ hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
 size_t split_workspace_bytes(int N, int D, int K, int64_t B);
 hipError_t launch_solve_split(int N, const SolveArgs& a, void* workspace, hipStream_t stream);
 
+// cost / gradient of fixed vertex derivatives at candidate times (mtg_cost.hip)
+size_t cost_lds_bytes(int N, int D, int K);
+hipError_t launch_cost_at_times(int N, int r, const double* values, const uint8_t* mask, const double* times,
+                                const double* scales, double* cost, double* grad, int64_t B, int K, int D, int C,
+                                hipStream_t stream);
+
 // evaluateRange
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
                              double t_end, double dt, int64_t* counts, hipStream_t stream);

@@ -103,6 +103,24 @@ class Context:
                 nat.check(rc, handle)
         return call
 
+    def cost_call(self, N, r, vertex_values, times, scales, cost):
+        """Zero-argument callable: one asynchronous device-pointer mtg_cost_at_times_batch launch on
+        torch's current stream (the config-5 bench step)."""
+        import torch
+        B, V, h, D = vertex_values.shape
+        C = scales.shape[0]
+        self.set_stream(torch.cuda.current_stream(vertex_values.device).cuda_stream)
+        fn = self._lib.mtg_cost_at_times_batch
+        args = (self.handle, N, D, V - 1, r, B, _addr(vertex_values), None, _addr(times), C, _addr(scales),
+                _addr(cost), None, nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC)
+        handle = self.handle
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                nat.check(rc, handle)
+        return call
+
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
                            cost=None, status=None, split=False, asynchronous=False, general=False):
@@ -182,6 +200,26 @@ class Context:
         nat.check(rc, self.handle)
         return cost
 
+    def cost_at_times_batch(self, N, r, vertex_values, times, scales, mask=None, grad=False):
+        """getCostAndGradientDerivative at candidate times (include/mtg.h mtg_cost_at_times_batch):
+        cost [B][C] = sum_dims d^T R(T_c) d, and with grad=True (needs mask) grad [B][C][D][V*h] =
+        2 (R(T_c) d)_free in the reference's free order.  scales [C][K] multiply times [B][K]."""
+        vertex_values = np.ascontiguousarray(vertex_values, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        scales = np.ascontiguousarray(scales, dtype=np.float64)
+        B, V, h, D = vertex_values.shape
+        K = V - 1
+        C = scales.shape[0]
+        assert scales.shape == (C, K) and times.shape == (B, K)
+        cost = np.empty((B, C))
+        g = np.zeros((B, C, D, V * h)) if grad else None
+        m = np.ascontiguousarray(mask, dtype=np.uint8) if mask is not None else None
+        self.reset_stream()
+        nat.check(self._lib.mtg_cost_at_times_batch(self.handle, N, D, K, r, B, _addr(vertex_values), _addr(m),
+                                                    _addr(times), C, _addr(scales), _addr(cost), _addr(g), 0),
+                  self.handle)
+        return (cost, g) if grad else cost
+
     # ------------------------------------------------------- evaluateRange
     def evaluate_range_batch(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True):
         """Host-array convenience wrapper: returns (samples [S][D], sample_times [S], counts [B], offsets [B])."""
@@ -203,6 +241,20 @@ class Context:
                                                      t_end, dt, derivative, _addr(counts), _addr(offsets),
                                                      _addr(out), _addr(st), 0), self.handle)
         return out[:total], (st[:total] if want_times else None), counts, offsets
+
+
+def full_vertex_values(values, mask, free, N):
+    """All derivatives of every vertex [B][V][h][D]: the fixed values where the mask says fixed,
+    the solved free values (free_out [B][D][V*h], reference order) elsewhere."""
+    values = np.asarray(values, dtype=np.float64)
+    B, V, h, D = values.shape
+    fixed = ((np.asarray(mask)[:, :, None] >> np.arange(h)[None, None, :]) & 1).astype(bool)  # [B][V][h]
+    out = np.where(fixed[..., None], values, 0.0)
+    for b in range(B):
+        slots = np.flatnonzero(~fixed[b].reshape(-1))  # (v, k) of free derivatives, reference order
+        for d in range(D):
+            out[b].reshape(-1, D)[slots, d] = free[b, d, :len(slots)]
+    return out
 
 
 _default_ctx = {}

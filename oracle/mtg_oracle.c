@@ -585,3 +585,59 @@ int64_t oracle_evaluate_range(int N, int D, int K, const double* coeffs, const d
   }
   return n;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Cost of fixed vertex derivatives at candidate times (config 5 CPU side)  */
+/* ------------------------------------------------------------------------ */
+int oracle_cost_at_times_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
+                               const double* times, int C, const double* scales, double* J,
+                               int threads) {
+  if (N < 2 || N > ORACLE_KMAXN || (N % 2) || K < 1 || D < 1 || C < 1 || nd < N / 2) return ORACLE_ERR_ARG;
+  const int h = N / 2, V = K + 1;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t b = 0; b < B; ++b) {
+    double A[ORACLE_KMAXN * ORACLE_KMAXN], Ai[ORACLE_KMAXN * ORACLE_KMAXN], Q[ORACLE_KMAXN * ORACLE_KMAXN];
+    double T1[ORACLE_KMAXN * ORACLE_KMAXN], H[ORACLE_KMAXN * ORACLE_KMAXN];
+    const double* x = xfull + (size_t)b * V * nd * D;
+    for (int c = 0; c < C; ++c) {
+      double cost = 0.0;
+      for (int i = 0; i < K; ++i) {
+        const double T = times[(size_t)b * K + i] * scales[(size_t)c * K + i];
+        /* updateSegmentTimes: A, A^-1 (Schur), Q; then H = A^-T Q A^-1 as constructR forms it */
+        oracle_setup_mapping_matrix(N, T, A);
+        oracle_invert_mapping_matrix(N, A, Ai);
+        oracle_quadratic_cost_jacobian(N, r, T, Q);
+        for (int p = 0; p < N; ++p)
+          for (int q = 0; q < N; ++q) {
+            double s = 0.0;
+            for (int k = 0; k < N; ++k) s += Q[p * N + k] * Ai[k * N + q];
+            T1[p * N + q] = s;
+          }
+        for (int p = 0; p < N; ++p)
+          for (int q = 0; q < N; ++q) {
+            double s = 0.0;
+            for (int k = 0; k < N; ++k) s += Ai[k * N + p] * T1[k * N + q];
+            H[p * N + q] = s;
+          }
+        for (int d = 0; d < D; ++d) {
+          double xs[ORACLE_KMAXN];
+          for (int k = 0; k < h; ++k) {
+            xs[k] = x[((size_t)i * nd + k) * D + d];
+            xs[h + k] = x[((size_t)(i + 1) * nd + k) * D + d];
+          }
+          for (int p = 0; p < N; ++p) {
+            double s = 0.0;
+            for (int q = 0; q < N; ++q) s += H[p * N + q] * xs[q];
+            cost += xs[p] * s;
+          }
+        }
+      }
+      J[(size_t)b * C + c] = cost;
+    }
+  }
+  (void)threads;
+  return ORACLE_OK;
+}

@@ -98,6 +98,13 @@ int oracle_solve_linear(const oracle_problem* p, oracle_outputs* out);
 void oracle_setup_mapping_matrix(int N, double T, double* A);
 void oracle_invert_mapping_matrix(int N, const double* A, double* Ainv);
 void oracle_quadratic_cost_jacobian(int N, int derivative, double T, double* Q);
+/* getCostAndGradientDerivative (polynomial_optimization_nonlinear_impl.h:1452-1520) at candidate
+ * times: J[b][c] = sum_dims d^T R(T_c) d with the reference's per-segment H = A^-T Q A^-1
+ * (updateSegmentTimes lin_impl:276-295), T_c[i] = times[b][i] * scales[c][i].
+ * xfull [B][V][nd][D] holds every derivative (fixed and solved free) of every vertex. */
+int oracle_cost_at_times_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
+                               const double* times, int C, const double* scales, double* J,
+                               int threads);
 
 /* Batched convenience for the CPU baseline: B problems with identical shape,
  * values [B][V][nd][D] etc.  Runs on `threads` OpenMP threads (<=0: all). */

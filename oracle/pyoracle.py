@@ -81,6 +81,8 @@ def lib(path=None):
                                         ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                         ctypes.c_int64, _dp, _dp]
     L.oracle_evaluate_range.restype = ctypes.c_int64
+    L.oracle_cost_at_times_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int64, _dp, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int]
     if path is None or _LIB is None:
         _LIB = L
     return L
@@ -228,3 +230,17 @@ def evaluate_range(coeffs, times, t_start, t_end, dt, derivative=0, max_samples=
                                     max_samples, _p(out), _p(st))
     m = min(n, max_samples)
     return out[:m], st[:m], n
+
+
+def cost_at_times_batch(N, r, xfull, times, scales, threads=0):
+    """getCostAndGradientDerivative's J at candidate times (oracle_cost_at_times_batch).
+    xfull [B][V][nd][D], times [B][K], scales [C][K] -> J [B][C]."""
+    xfull = np.ascontiguousarray(xfull, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    scales = np.ascontiguousarray(scales, dtype=np.float64)
+    B, V, nd, D = xfull.shape
+    C = scales.shape[0]
+    J = np.zeros((B, C))
+    rc = lib().oracle_cost_at_times_batch(N, D, V - 1, r, nd, B, _p(xfull), _p(times), C, _p(scales), _p(J), threads)
+    assert rc == 0, rc
+    return J

@@ -237,3 +237,53 @@ def test_evaluate_range_vs_oracle(gpu_ctx):
                 assert n == counts[b]
                 np.testing.assert_array_equal(st[offs[b]:offs[b] + n], rst)
                 np.testing.assert_array_equal(out[offs[b]:offs[b] + n], ro)
+
+
+def _oracle_cost_grad(N, r, xfull, mask, times):
+    """Reference getCostAndGradientDerivative (nl_impl:1452-1520) from the oracle's FP64 per-segment
+    H = A^-T Q A^-1 (lin_impl:133-169, :574-589): J = sum d^T R d, grad = 2 (R d)_free."""
+    O = _oracle()
+    V, h, D = xfull.shape
+    K = V - 1
+    J = 0.0
+    Rd = np.zeros((V, h, D))
+    for i in range(K):
+        Ai = O.invert_mapping_matrix(O.setup_mapping_matrix(N, times[i]))
+        Hm = Ai.T @ O.quadratic_cost_jacobian(N, r, times[i]) @ Ai
+        x = np.concatenate([xfull[i], xfull[i + 1]], axis=0)  # [N][D]
+        y = Hm @ x
+        J += float(np.sum(x * y))
+        Rd[i] += y[:h]
+        Rd[i + 1] += y[h:]
+    free = ~(((mask[:, None] >> np.arange(h)[None, :]) & 1).astype(bool))
+    g = np.stack([2.0 * Rd[..., d][free] for d in range(D)])  # [D][n_free]
+    return J, g
+
+
+def test_cost_at_times_vs_oracle(gpu_ctx):
+    """Config 5 ingredients: J(T_c) at fixed solved derivatives for 64 candidate allocations, and
+    the gradient 2 (R d)_free; at the solved times the gradient vanishes (optimality) and J equals
+    2 x computeCost."""
+    from mav_trajectory_generation_cmake_amd import full_vertex_values
+    B, K, N, r = 16, 10, 10, 4
+    vals, mask, times = _bench_batch(B, seed0=21, K=K)
+    sol = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, free=True, cost=True)
+    xfull = full_vertex_values(vals, mask, sol["free"], N)
+    rng = np.random.default_rng(0)
+    C = 64
+    scales = np.repeat((0.5 + np.arange(C) / 63.0)[:, None], K, axis=1)
+    scales[1::2] *= rng.uniform(0.8, 1.2, size=(C // 2, K))  # per-segment jitter on odd candidates
+    scales[0] = 1.0
+    J, g = gpu_ctx.cost_at_times_batch(N, r, xfull, times, scales, mask=mask, grad=True)
+    np.testing.assert_allclose(J[:, 0], 2.0 * sol["cost"], rtol=1e-9)
+    for b in range(4):
+        for c in (0, 1, 17, 63):
+            Jr, gr = _oracle_cost_grad(N, r, xfull[b], mask[b], times[b] * scales[c])
+            assert abs(J[b, c] - Jr) <= 1e-7 * abs(Jr), (b, c, J[b, c], Jr)
+            nf = gr.shape[1]
+            scale = np.max(np.abs(gr)) if c else np.max(np.abs(_oracle_cost_grad(N, r, xfull[b], mask[b],
+                                                                                 times[b] * scales[1])[1]))
+            assert np.max(np.abs(g[b, c, :, :nf] - gr)) <= 1e-6 * scale, (b, c)
+    # optimality at the solved times: 2 (R d)_free = 0 up to rounding
+    g1 = np.abs(g[:, 1]).max(axis=(1, 2))
+    assert np.all(np.abs(g[:, 0]).max(axis=(1, 2)) <= 1e-6 * g1)

@@ -221,3 +221,23 @@ def test_evaluate_range_semantics():
     assert st2[0] == 1.0 and n2 == 4
     # start beyond the end: nothing
     assert O.evaluate_range(c, t, 10.0, 11.0, 0.1)[2] == 0
+
+
+def test_cost_at_times_oracle_consistency():
+    """getCostAndGradientDerivative's J = sum d^T R d (nl_impl:1452-1520) at the solved times is
+    2 x computeCost (lin_impl:114-130); scaling all times by s scales the cost of the SAME
+    derivatives as expected; full_vertex_values rebuilds d in the reference's free order."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, 10, 6, seed0=40)
+    free = np.zeros((6, 3, 55))
+    cost = np.zeros(6)
+    for b in range(6):
+        r = O.solve_linear(10, 4, vals[b], mask[b].astype(np.uint32), times[b])
+        free[b, :, :r["n_free"]] = r["free"]
+        cost[b] = r["cost"]
+    xf = mtg.full_vertex_values(vals, mask, free, 10)
+    fixed = ((mask[:, :, None] >> np.arange(5)) & 1).astype(bool)
+    np.testing.assert_array_equal(xf[fixed], vals[fixed])
+    J = O.cost_at_times_batch(10, 4, xf, times, np.array([[1.0] * 10, [2.0] * 10]))
+    np.testing.assert_allclose(J[:, 0], 2 * cost, rtol=1e-9)
+    assert np.all(J[:, 1] > 0) and np.all(np.isfinite(J[:, 1]))
