@@ -113,8 +113,9 @@ int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_
  * trajectories, with the reference's sequential time accumulation (acc += dt)
  * reproduced exactly.  coeffs [B][K][D][N], times [B][K].  Sample counts are
  * ragged: first call with out == NULL to get counts[B] (samples per
- * trajectory); then pass offsets[B] (exclusive prefix sum of counts, in
- * samples) and out [sum(counts)][D] (+ optional sample_times [sum]).
+ * trajectory); then pass the same counts (read), offsets[B] (exclusive prefix
+ * sum of counts, in samples) and out [sum(counts)][D] (+ optional
+ * sample_times [sum]).
  * t_start/t_end/dt are shared by the whole batch; derivative selects the
  * derivative order evaluated (Polynomial::evaluate, polynomial.h:138-151). */
 int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,

@@ -413,7 +413,7 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
     } else {
       MTG_HIP_TRY(ctx, time_begin(ctx));
       MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative,
-                                              offsets, out, sample_times, ctx->stream));
+                                              counts, offsets, out, sample_times, ctx->stream));
       MTG_HIP_TRY(ctx, time_end(ctx));
     }
     if (!(flags & MTG_FLAG_ASYNC)) MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -446,10 +446,12 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
   } else {
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coeffs, coeffs, b_coeffs, hipMemcpyHostToDevice, ctx->stream));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_offsets, offsets, b_counts, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_counts, counts, b_counts, hipMemcpyHostToDevice, ctx->stream));
     MTG_HIP_TRY(ctx, time_begin(ctx));
     MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<double*>(base + o_coeffs),
                                             reinterpret_cast<double*>(base + o_times), t_start, t_end, dt,
-                                            derivative, reinterpret_cast<int64_t*>(base + o_offsets),
+                                            derivative, reinterpret_cast<int64_t*>(base + o_counts),
+                                            reinterpret_cast<int64_t*>(base + o_offsets),
                                             reinterpret_cast<double*>(base + o_out),
                                             sample_times ? reinterpret_cast<double*>(base + o_st) : nullptr,
                                             ctx->stream));

@@ -62,53 +62,101 @@ __global__ void eval_count_kernel(int K, int64_t B, const double* times, double 
   counts[b] = n;
 }
 
+// Samples per chunk (one wave: lane l evaluates sample 64 c + l) and chunks checkpointed per round.
+constexpr int kChunk = 64;
+constexpr int kRoundChunks = 256;
+constexpr int kEvalThreads = 256;
+
+// One workgroup per trajectory.  Lane 0 replays the reference's clock (exactly the recurrence
+// above) and checkpoints (acc, tin, segment) at every 64th sample into LDS; then every lane
+// replays at most 63 steps from its chunk's checkpoint -- the same floating-point operations in
+// the same order, so sample times and segment choices stay bit-identical -- and evaluates its
+// sample.  The trajectory's coefficients are staged in LDS; output rows are contiguous per wave.
 template <int N>
-__global__ void eval_range_kernel(int D, int K, int64_t B, const double* coeffs, const double* times,
-                                  double t_start, double t_end, double dt, int derivative,
-                                  const int64_t* offsets, double* out, double* sample_times) {
+__global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, const double* coeffs,
+                                                                  const double* times, double t_start, double dt,
+                                                                  int derivative, const int64_t* counts,
+                                                                  const int64_t* offsets, double* out,
+                                                                  double* sample_times) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
   // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
 #pragma clang fp contract(off)
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const double* tms = times + b * K;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t n_total = counts[b];
+  if (n_total <= 0) return;
+  double* cf = lds;                               // [K][D][N]
+  double* tl = cf + K * D * N;                    // [K]
+  double* ck_acc = tl + K;                        // [kRoundChunks]
+  double* ck_tin = ck_acc + kRoundChunks;         // [kRoundChunks]
+  int* ck_seg = reinterpret_cast<int*>(ck_tin + kRoundChunks);
   const double* cb = coeffs + b * (int64_t)K * D * N;
+  for (int i = tid; i < K * D * N; i += kEvalThreads) cf[i] = cb[i];
+  for (int i = tid; i < K; i += kEvalThreads) tl[i] = times[b * K + i];
   double row[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) row[j] = base_coeff(derivative, j);
-  int i;
-  double acc, tin;
-  if (!range_start(tms, K, t_start, &i, &acc, &tin)) return;
-  int64_t n = offsets[b];
-  while (acc < t_end) {
-    if (tin > tms[i]) {
-      tin = tin - tms[i];
-      if (++i >= K) break;
-      continue;
-    }
-    const double* cs = cb + (int64_t)i * D * N;
-    for (int d = 0; d < D; ++d) {
-      double v = 0.0;
-      if (derivative < N) {
-        const double* c = cs + d * N;
-        // result = row[N-1] c[N-1]; result *= t; result += row[j] c[j]: plain operators under
-        // the contract(off) pragma above, so the rounding is the reference's multiply-then-add
-        // (the pragma does not reach into inlined helpers such as __dmul_rn)
-        v = row[N - 1] * c[N - 1];
-#pragma unroll
-        for (int j = N - 2; j >= 0; --j) {
-          if (j >= derivative) {
-            v = v * tin;
-            v = v + row[j] * c[j];
+  const int64_t base = offsets[b];
+  // lane 0's running clock (state before the switch check of sample n)
+  int seg = 0;
+  double acc = 0.0, tin = 0.0;
+  if (tid == 0) range_start(times + b * K, K, t_start, &seg, &acc, &tin);
+  __syncthreads();
+  const int wave = tid / kChunk, lane = tid % kChunk;
+  for (int64_t n0 = 0; n0 < n_total; n0 += (int64_t)kRoundChunks * kChunk) {
+    const int64_t left = n_total - n0;
+    const int nch = (int)((left + kChunk - 1) / kChunk < kRoundChunks ? (left + kChunk - 1) / kChunk : kRoundChunks);
+    if (tid == 0) {
+      for (int c = 0; c < nch; ++c) {
+        ck_acc[c] = acc;
+        ck_tin[c] = tin;
+        ck_seg[c] = seg;
+        for (int s = 0; s < kChunk; ++s) {  // advance one chunk: 64 emitted samples
+          while (tin > tl[seg] && seg < K - 1) {
+            tin = tin - tl[seg];
+            ++seg;
           }
+          tin += dt;
+          acc += dt;
         }
       }
-      out[n * D + d] = v;
     }
-    if (sample_times) sample_times[n] = acc;
-    ++n;
-    tin += dt;
-    acc += dt;
+    __syncthreads();
+    for (int c = wave; c < nch; c += kEvalThreads / kChunk) {
+      const int64_t n = n0 + (int64_t)c * kChunk + lane;
+      double a = ck_acc[c], t = ck_tin[c];
+      int i = ck_seg[c];
+      for (int s = 0;; ++s) {
+        while (t > tl[i] && i < K - 1) {
+          t = t - tl[i];
+          ++i;
+        }
+        if (s == lane) break;
+        t += dt;
+        a += dt;
+      }
+      if (n < n_total) {
+        const double* cs = cf + (i * D) * N;
+        for (int d = 0; d < D; ++d) {
+          double v = 0.0;
+          if (derivative < N) {
+            const double* c = cs + d * N;
+            v = row[N - 1] * c[N - 1];
+#pragma unroll
+            for (int j = N - 2; j >= 0; --j) {
+              if (j >= derivative) {
+                v = v * t;
+                v = v + row[j] * c[j];
+              }
+            }
+          }
+          out[(base + n) * D + d] = v;
+        }
+        if (sample_times) sample_times[base + n] = a;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -125,15 +173,16 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
 }
 
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs, const double* times,
-                             double t_start, double t_end, double dt, int derivative,
+                             double t_start, double t_end, double dt, int derivative, const int64_t* counts,
                              const int64_t* offsets, double* out, double* sample_times, hipStream_t stream) {
-  const int block = 64;
-  const int64_t grid = (B + block - 1) / block;
-  if (grid == 0) return hipSuccess;
-#define MTG_EVAL_CASE(NN)                                                                          \
-  case NN:                                                                                         \
-    hipLaunchKernelGGL(eval_range_kernel<NN>, dim3((unsigned)grid), dim3(block), 0, stream, D, K, B, \
-                       coeffs, times, t_start, t_end, dt, derivative, offsets, out, sample_times); \
+  (void)t_end;  // the sample counts (eval_count_kernel) already encode t_end
+  if (B == 0) return hipSuccess;
+  const size_t lds = sizeof(double) * ((size_t)K * D * N + K + 2 * kRoundChunks) + sizeof(int) * kRoundChunks;
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+#define MTG_EVAL_CASE(NN)                                                                               \
+  case NN:                                                                                              \
+    hipLaunchKernelGGL(eval_range_kernel<NN>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, \
+                       coeffs, times, t_start, dt, derivative, counts, offsets, out, sample_times);     \
     break;
   switch (N) {
     MTG_EVAL_CASE(2)

@@ -50,7 +50,7 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
                              double t_end, double dt, int64_t* counts, hipStream_t stream);
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs,
                              const double* times, double t_start, double t_end, double dt,
-                             int derivative, const int64_t* offsets, double* out,
+                             int derivative, const int64_t* counts, const int64_t* offsets, double* out,
                              double* sample_times, hipStream_t stream);
 
 }  // namespace mtg
