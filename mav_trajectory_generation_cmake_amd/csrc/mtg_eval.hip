@@ -2,10 +2,24 @@
 //
 // The reference advances its clock by repeated FP addition (acc += dt,
 // tin += dt, tin -= T_i at a segment switch, :109-126), so the number of
-// samples and every sample time depend on the sequential rounding.  These
-// kernels replay exactly that recurrence per trajectory (bit-identical sample
-// times and counts) and evaluate the segment polynomials with the
-// reference's Horner form (Polynomial::evaluate, polynomial.h:138-151).
+// samples and every sample time depend on the sequential rounding.  Replaying
+// that chain sample by sample costs ~80 cycles of FP64 latency per sample on
+// gfx950 (scripts/micro/f64_latency.hip), ~0.6 M cycles per trajectory.
+//
+// These kernels reproduce it exactly without the chain.  While a positive
+// double x stays inside one binade [2^e, 2^(e+1)), its grid spacing u is
+// fixed, so fl(x + dt) = x + inc u with a constant integer inc = RNE(dt / u)
+// (when dt / u is an exact half-integer, once the mantissa is even the tie
+// always resolves to inc = q + (q & 1)).  The clock therefore splits into
+// "runs": maximal ranges of samples on which tin and acc are both such
+// progressions, ended by a binade crossing of either, a segment switch or
+// t_end -- each found in closed form with integer arithmetic.  The step that
+// ends a run is done as a real FP addition, so every state is the
+// reference's.  A trajectory has ~10 runs per segment instead of ~750
+// sequential steps; within a run every sample's (acc, tin) is
+// (m + k inc) 2^E, which makes the evaluation fully parallel.  The segment
+// polynomials use the reference's Horner form (Polynomial::evaluate,
+// polynomial.h:138-151), multiply-then-add.
 #include <float.h>
 
 #include "mtg_internal.h"
@@ -39,43 +53,186 @@ __device__ __forceinline__ bool range_start(const double* tms, int K, double t_s
   return true;
 }
 
+// x_k = (m + k inc) 2^E, k = 0, 1, ...: the values fl(x + dt) takes while x stays in its binade.
+struct Prog {
+  int64_t m, inc;
+  int E;
+};
+
+constexpr int64_t kTwo53 = 9007199254740992LL;
+
+// floor(num / den) for 0 <= num < 2^62, 0 < den < 2^62: v_rcp_f64 refined by one Newton step
+// (multiply and subtract, not fused), then corrected to the exact integer quotient.  ~4x cheaper
+// than the int64 division emulation, and the run arithmetic is the serial part of the clock.
+__device__ __forceinline__ int64_t floor_div(int64_t num, int64_t den) {
+#pragma clang fp contract(off)
+  const double dd = (double)den;
+  double y = __builtin_amdgcn_rcp(dd);
+  y = y * (2.0 - dd * y);
+  double qd = (double)num * y;
+  if (qd > 4.0e18) qd = 4.0e18;
+  int64_t q = (int64_t)qd;
+  if (q < 0) q = 0;
+  while (q > 0 && q * den > num) --q;
+  while ((q + 1) * den <= num) ++q;
+  return q;
+}
+
+// (m + k inc) 2^E with m + k inc in [2^52, 2^53): the double is assembled from its bit fields
+__device__ __forceinline__ double mant_exp(int64_t v, int E) {
+  return __longlong_as_double(((int64_t)(E + 1075) << 52) | (v - (int64_t)(1ll << 52)));
+}
+
+// The progression of x under x <- fl(x + dt), if x is a normal positive double whose first step
+// stays in its binade and is not an unresolved tie (odd mantissa).  Otherwise false: the caller
+// takes one real step.
+__device__ __forceinline__ bool progression(double x, double dt, Prog* p) {
+  if (!(x > 0.0)) return false;
+  const uint64_t bits = (uint64_t)__double_as_longlong(x);
+  const int ex = (int)((bits >> 52) & 0x7FF);
+  if (ex == 0 || ex == 0x7FF) return false;
+  const int64_t m = (int64_t)((bits & ((1ull << 52) - 1)) | (1ull << 52));
+  const int E = ex - 1075;
+  const double f = __builtin_amdgcn_ldexp(dt, -E);  // dt / u, exact (power-of-two scaling)
+  if (!(f < (double)(kTwo53 - m))) return false;     // the first step leaves the binade
+  const double q = __builtin_floor(f);
+  const double phi = f - q;
+  const int64_t qi = (int64_t)q;
+  int64_t inc;
+  if (phi < 0.5) {
+    inc = qi;
+  } else if (phi > 0.5) {
+    inc = qi + 1;
+  } else {
+    if (m & 1) return false;  // tie from an odd mantissa: one real step makes it even
+    inc = qi + (qi & 1);
+  }
+  if (inc <= 0) return false;
+  p->m = m;
+  p->inc = inc;
+  p->E = E;
+  return true;
+}
+
+__device__ __forceinline__ double prog_value(const Prog& p, int64_t k) { return mant_exp(p.m + k * p.inc, p.E); }
+
+constexpr int64_t kNoLimit = (int64_t)1 << 62;
+
+// number of k >= 0 with m + k inc <= lim (lim given as a double, exact if < 2^62, else no limit)
+__device__ __forceinline__ int64_t run_len_le(const Prog& p, double lim_scaled) {
+  if (!(lim_scaled < 4.0e18)) return kNoLimit;
+  const int64_t lim = (int64_t)lim_scaled;
+  if (lim < p.m) return 0;
+  return floor_div(lim - p.m, p.inc) + 1;
+}
+
+// One run of the clock: samples n0 .. n0+L-1 at tin = prog_value(t, k), acc = prog_value(a, k)
+// (L == 1 and single: the plain doubles tin0 / acc0), all in segment seg.
+struct Run {
+  int64_t n0, L;
+  Prog t, a;
+  double tin0, acc0;
+  int seg;
+  bool single;
+};
+
+// The reference's clock (src/trajectory.cpp:86-127), advanced run by run.
+struct Clock {
+  const double* T;
+  int K;
+  double dt, t_end;
+  double acc, tin, Ti;
+  int seg;
+  int64_t n;
+  bool done;
+
+  __device__ __forceinline__ void init(const double* tms, int K_, double t_start, double t_end_, double dt_) {
+    T = tms;
+    K = K_;
+    dt = dt_;
+    t_end = t_end_;
+    n = 0;
+    done = !range_start(tms, K, t_start, &seg, &acc, &tin);
+    Ti = done ? 0.0 : T[seg];
+  }
+
+  // next run into *r; false when the clock has stopped
+  __device__ __forceinline__ bool next(Run* r) {
+    while (!done) {
+      if (!(acc < t_end)) {
+        done = true;
+        break;
+      }
+      if (tin > Ti) {  // segment switch: no sample, acc unchanged
+        tin = tin - Ti;
+        if (++seg >= K) {
+          done = true;
+          break;
+        }
+        Ti = T[seg];
+        continue;
+      }
+      r->n0 = n;
+      r->seg = seg;
+      r->tin0 = tin;
+      r->acc0 = acc;
+      Prog pt, pa;
+      int64_t L = 1;
+      r->single = true;
+      if (progression(tin, dt, &pt) && progression(acc, dt, &pa)) {
+        int64_t lim = floor_div(kTwo53 - 1 - pt.m, pt.inc) + 1;                             // tin binade
+        lim = min(lim, floor_div(kTwo53 - 1 - pa.m, pa.inc) + 1);                              // acc binade
+        lim = min(lim, run_len_le(pt, __builtin_amdgcn_ldexp(Ti, -pt.E)));                     // tin <= T_i
+        const double q = __builtin_amdgcn_ldexp(t_end, -pa.E);                                 // acc < t_end
+        if (q < 4.0e18) lim = min(lim, run_len_le(pa, __builtin_ceil(q) - 1.0));
+        L = lim < 1 ? 1 : lim;
+        r->t = pt;
+        r->a = pa;
+        r->single = false;
+        if (L > 1) {  // state at the run's last sample, exactly
+          tin = prog_value(pt, L - 1);
+          acc = prog_value(pa, L - 1);
+        }
+      }
+      r->L = L;
+      n += L;
+      tin += dt;  // the step after the run's last sample, as the reference takes it
+      acc += dt;
+      return true;
+    }
+    return false;
+  }
+};
+
 __global__ void eval_count_kernel(int K, int64_t B, const double* times, double t_start, double t_end,
                                   double dt, int64_t* counts) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const double* tms = times + b * K;
-  int i;
-  double acc, tin;
-  int64_t n = 0;
-  if (range_start(tms, K, t_start, &i, &acc, &tin)) {
-    while (acc < t_end) {
-      if (tin > tms[i]) {
-        tin = tin - tms[i];
-        if (++i >= K) break;
-        continue;
-      }
-      ++n;
-      tin += dt;
-      acc += dt;
-    }
+  Clock ck;
+  ck.init(times + b * K, K, t_start, t_end, dt);
+  Run r;
+  while (ck.next(&r)) {
   }
-  counts[b] = n;
+  counts[b] = ck.n;
 }
 
-// Samples per chunk (one wave: lane l evaluates sample 64 c + l) and chunks checkpointed per round.
-constexpr int kChunk = 64;
-constexpr int kRoundChunks = 256;
-constexpr int kEvalThreads = 256;
+// Runs per round of the LDS table (built by lane 0, consumed by the wave).
+constexpr int kRuns = 64;
+constexpr int kEvalThreads = 64;
 
-// One workgroup per trajectory.  Lane 0 replays the reference's clock (exactly the recurrence
-// above) and checkpoints (acc, tin, segment) at every 64th sample into LDS; then every lane
-// replays at most 63 steps from its chunk's checkpoint -- the same floating-point operations in
-// the same order, so sample times and segment choices stay bit-identical -- and evaluates its
-// sample.  The trajectory's coefficients are staged in LDS; output rows are contiguous per wave.
+struct RunLds {  // structure of arrays in LDS
+  int64_t n0[kRuns], L[kRuns], tm[kRuns], ti[kRuns], am[kRuns], ai[kRuns];
+  double tin0[kRuns], acc0[kRuns];
+  int tE[kRuns], aE[kRuns], seg[kRuns], single[kRuns];
+};
+
+// One wave per trajectory: lane 0 turns the clock into runs (a few tens per segment), all lanes
+// evaluate the runs' samples -- consecutive samples on consecutive lanes -- with the coefficients
+// staged in LDS.
 template <int N>
 __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, const double* coeffs,
-                                                                  const double* times, double t_start, double dt,
-                                                                  int derivative, const int64_t* counts,
+                                                                  const double* times, double t_start, double t_end,
+                                                                  double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
                                                                   double* sample_times) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
@@ -83,80 +240,88 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const int64_t b = blockIdx.x;
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int64_t n_total = counts[b];
   if (n_total <= 0) return;
-  double* cf = lds;                               // [K][D][N]
-  double* tl = cf + K * D * N;                    // [K]
-  double* ck_acc = tl + K;                        // [kRoundChunks]
-  double* ck_tin = ck_acc + kRoundChunks;         // [kRoundChunks]
-  int* ck_seg = reinterpret_cast<int*>(ck_tin + kRoundChunks);
+  RunLds* rt = reinterpret_cast<RunLds*>(lds);
+  double* cf = reinterpret_cast<double*>(rt + 1);  // [K][D][N]
+  double* ob = cf + K * D * N;                     // [kEvalThreads][D] output block
   const double* cb = coeffs + b * (int64_t)K * D * N;
-  for (int i = tid; i < K * D * N; i += kEvalThreads) cf[i] = cb[i];
-  for (int i = tid; i < K; i += kEvalThreads) tl[i] = times[b * K + i];
+  for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = cb[i];
   double row[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) row[j] = base_coeff(derivative, j);
   const int64_t base = offsets[b];
-  // lane 0's running clock (state before the switch check of sample n)
-  int seg = 0;
-  double acc = 0.0, tin = 0.0;
-  if (tid == 0) range_start(times + b * K, K, t_start, &seg, &acc, &tin);
-  __syncthreads();
-  const int wave = tid / kChunk, lane = tid % kChunk;
-  for (int64_t n0 = 0; n0 < n_total; n0 += (int64_t)kRoundChunks * kChunk) {
-    const int64_t left = n_total - n0;
-    const int nch = (int)((left + kChunk - 1) / kChunk < kRoundChunks ? (left + kChunk - 1) / kChunk : kRoundChunks);
-    if (tid == 0) {
-      for (int c = 0; c < nch; ++c) {
-        ck_acc[c] = acc;
-        ck_tin[c] = tin;
-        ck_seg[c] = seg;
-        for (int s = 0; s < kChunk; ++s) {  // advance one chunk: 64 emitted samples
-          while (tin > tl[seg] && seg < K - 1) {
-            tin = tin - tl[seg];
-            ++seg;
-          }
-          tin += dt;
-          acc += dt;
-        }
+  Clock ck;
+  if (lane == 0) ck.init(times + b * K, K, t_start, t_end, dt);
+  __shared__ int s_nr;
+  __shared__ int64_t s_end;
+  for (;;) {
+    if (lane == 0) {
+      int nr = 0;
+      Run r;
+      while (nr < kRuns && ck.next(&r)) {
+        rt->n0[nr] = r.n0;
+        rt->L[nr] = r.L;
+        rt->tm[nr] = r.t.m;
+        rt->ti[nr] = r.t.inc;
+        rt->tE[nr] = r.t.E;
+        rt->am[nr] = r.a.m;
+        rt->ai[nr] = r.a.inc;
+        rt->aE[nr] = r.a.E;
+        rt->tin0[nr] = r.tin0;
+        rt->acc0[nr] = r.acc0;
+        rt->seg[nr] = r.seg;
+        rt->single[nr] = r.single;
+        ++nr;
       }
+      s_nr = nr;
+      s_end = ck.n;
     }
     __syncthreads();
-    for (int c = wave; c < nch; c += kEvalThreads / kChunk) {
-      const int64_t n = n0 + (int64_t)c * kChunk + lane;
-      double a = ck_acc[c], t = ck_tin[c];
-      int i = ck_seg[c];
-      for (int s = 0;; ++s) {
-        while (t > tl[i] && i < K - 1) {
-          t = t - tl[i];
-          ++i;
-        }
-        if (s == lane) break;
-        t += dt;
-        a += dt;
+    const int nr = s_nr;
+    if (nr == 0) break;
+    const int64_t first = rt->n0[0], end = s_end < n_total ? s_end : n_total;
+    int ri = 0;
+    for (int64_t nb = first; nb < end; nb += kEvalThreads) {
+      const int64_t n = nb + lane;
+      const int cnt = (int)(end - nb < kEvalThreads ? end - nb : kEvalThreads);
+      if (n < end) {
+      while (ri + 1 < nr && rt->n0[ri + 1] <= n) ++ri;
+      const int64_t k = n - rt->n0[ri];
+      double t, a;
+      if (rt->single[ri]) {
+        t = rt->tin0[ri];
+        a = rt->acc0[ri];
+      } else {
+        t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
+        a = mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]);
       }
-      if (n < n_total) {
-        const double* cs = cf + (i * D) * N;
-        for (int d = 0; d < D; ++d) {
-          double v = 0.0;
-          if (derivative < N) {
-            const double* c = cs + d * N;
-            v = row[N - 1] * c[N - 1];
+      const double* cs = cf + (rt->seg[ri] * D) * N;
+      for (int d = 0; d < D; ++d) {
+        double v = 0.0;
+        if (derivative < N) {
+          const double* c = cs + d * N;
+          v = row[N - 1] * c[N - 1];
 #pragma unroll
-            for (int j = N - 2; j >= 0; --j) {
-              if (j >= derivative) {
-                v = v * t;
-                v = v + row[j] * c[j];
-              }
+          for (int j = N - 2; j >= 0; --j) {
+            if (j >= derivative) {
+              v = v * t;
+              v = v + row[j] * c[j];
             }
           }
-          out[(base + n) * D + d] = v;
         }
-        if (sample_times) sample_times[base + n] = a;
+        ob[lane * D + d] = v;
       }
+      if (sample_times) sample_times[base + n] = a;
+      }
+      __syncthreads();
+      // the block's rows are contiguous in out: write them with consecutive lanes
+      double* dst = out + (base + nb) * D;
+      for (int i = lane; i < cnt * D; i += kEvalThreads) dst[i] = ob[i];
+      __syncthreads();
     }
-    __syncthreads();
+    if (end >= n_total) break;
   }
 }
 
@@ -175,14 +340,13 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs, const double* times,
                              double t_start, double t_end, double dt, int derivative, const int64_t* counts,
                              const int64_t* offsets, double* out, double* sample_times, hipStream_t stream) {
-  (void)t_end;  // the sample counts (eval_count_kernel) already encode t_end
   if (B == 0) return hipSuccess;
-  const size_t lds = sizeof(double) * ((size_t)K * D * N + K + 2 * kRoundChunks) + sizeof(int) * kRoundChunks;
+  const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
 #define MTG_EVAL_CASE(NN)                                                                               \
   case NN:                                                                                              \
     hipLaunchKernelGGL(eval_range_kernel<NN>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, \
-                       coeffs, times, t_start, dt, derivative, counts, offsets, out, sample_times);     \
+                       coeffs, times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times);     \
     break;
   switch (N) {
     MTG_EVAL_CASE(2)

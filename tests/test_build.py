@@ -34,4 +34,8 @@ def test_evaluate_range_has_no_fma(tmp_path):
     bodies = _kernel_bodies(_device_asm("mtg_eval.hip", tmp_path), r"_ZN3mtg17eval_range_kernel")
     assert len(bodies) == 6  # N = 2, 4, ..., 12
     for name, body in bodies.items():
-        assert not re.search(r"v_fma", body), name
+        # f64 FMAs are allowed only as the compiler's f64 -> int64 conversion idiom (x - 2^32 hi,
+        # constant 0xc1f00000) in the clock's integer run arithmetic; f32 FMAs belong to its
+        # integer-division emulation.  Any other f64 FMA would be a contracted Horner step.
+        bad = [ln for ln in body.splitlines() if re.search(r"v_fmac?_f64", ln) and "0xc1f00000" not in ln]
+        assert not bad, (name, bad[:3])
