@@ -13,8 +13,9 @@ Other workloads (--workload), each its own JSON line:
   config4  N=12, K=20, r=JERK: createRandomVertices(SNAP, 20, [-10,-20,-10], [10,20,10], seed)
            + estimateSegmentTimes(3, 5) (src/vertex.cpp:27-79, :162-178)
   config5  the config-2 problems, solved once (untimed), then one step = the cost of the solved
-           derivatives at 64 candidate time allocations (getCostAndGradientDerivative at
-           T_c = s_c T, s_c = 0.5 + c/63; mtg_cost_at_times_batch)
+           derivatives and its segment-time Jacobian at 64 candidate time allocations
+           (getCostAndGradientDerivative + getCostAndGradientTime's J_d gradient at T_c = s_c T,
+           s_c = 0.5 + c/63; mtg_time_jacobian_batch, v_mfma_f64_16x16x4_f64)
 
 Multi-GPU: one process per GPU (torchrun), contiguous shards, no data-path
 collective ("scaling": "weak"); a barrier + MAX-over-ranks of the timed region.
@@ -46,9 +47,11 @@ def algorithmic_bytes_per_traj(N, D, K):
 
 
 def cost_sweep_bytes_per_traj(N, D, K, C):
-    """mtg_cost_at_times_batch: vertex derivatives [V][h][D] + times [K] in, costs [C] out."""
+    """mtg_time_jacobian_batch: vertex derivatives [V][h][D] + times [K] in, costs [C] and the time
+    Jacobian [C][K] out (config 5: 1320 + 80 + 512 + 5120 = 7032 B; the candidate scales [C][K] are
+    shared by the batch)."""
     V, h = K + 1, N // 2
-    return V * h * D * 8 + K * 8 + C * 8
+    return V * h * D * 8 + K * 8 + C * 8 + C * K * 8
 
 
 def shard_seed0(rank, batch_per_rank):
@@ -105,13 +108,14 @@ def cpu_baseline(values, mask, times, N, r, target_s, threads):
 
 
 def cpu_baseline_cost(xfull, times, scales, N, r, target_s, threads):
-    """Oracle getCostAndGradientDerivative at candidate times: per candidate the reference's
-    updateSegmentTimes (A, Schur A^-1, Q) and d^T R d."""
+    """Oracle getCostAndGradientDerivative at candidate times with getCostAndGradientTime's J_d
+    gradient, as the reference computes it: per candidate the reference's per-segment H (A, Schur
+    A^-1, Q) and d^T R d, and per segment the central difference with increment_time 0.1."""
     pyoracle = _oracle_lib()
     done = 0
     t0 = time.perf_counter()
     while True:
-        pyoracle.cost_at_times_batch(N, r, xfull, times, scales, threads=threads)
+        pyoracle.cost_time_jacobian_batch(N, r, xfull, times, scales, 0.1, threads=threads)
         done += len(xfull) * len(scales)
         el = time.perf_counter() - t0
         if el >= target_s:
@@ -178,8 +182,9 @@ def main():
         x_d = torch.from_numpy(xfull).to(dev)
         s_d = torch.from_numpy(np.ascontiguousarray(scales)).to(dev)
         out_d = torch.empty((B, C5_CANDIDATES), dtype=torch.float64, device=dev)
-        step = ctx.cost_call(N, r, x_d, t_d, s_d, out_d)
-        kname = "cost_at_times_kernel"
+        jac_d = torch.empty((B, C5_CANDIDATES, K), dtype=torch.float64, device=dev)
+        step = ctx.jacobian_call(N, r, x_d, t_d, s_d, out_d, jac_d)
+        kname = "time_jacobian_kernel"
     else:
         out_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
         # one step = one launch of the solve on torch's current stream; the C ABI brackets every
@@ -217,13 +222,17 @@ def main():
 
     # spot check of the timed outputs (finite) -- not timed
     assert np.isfinite(out_d.cpu().numpy()).all(), "non-finite outputs"
+    if wl == "config5":
+        assert np.isfinite(jac_d.cpu().numpy()).all(), "non-finite Jacobian"
 
     if wl == "config5":
         units = B * C5_CANDIDATES
         bpt = cost_sweep_bytes_per_traj(N, D, K, C5_CANDIDATES)
-        metric = "trajectory-candidate costs/sec (config 5: 64 time allocations x 10-seg N=10 3-D)"
-        unit = "candidate costs/s"
-        workload = "config5: %d x 64 candidate allocations (K=%d, N=%d, D=%d, r=SNAP) per GPU, d fixed" % (B, K, N, D)
+        metric = ("trajectory-candidate cost+time-Jacobian evaluations/sec "
+                  "(config 5: 64 time allocations x 10-seg N=10 3-D)")
+        unit = "candidate evaluations/s"
+        workload = ("config5: %d x 64 candidate allocations (K=%d, N=%d, D=%d, r=SNAP) per GPU, d fixed; "
+                    "cost [B][64] + dJ/dT [B][64][K] (exact) on the matrix cores" % (B, K, N, D))
         data = ("synthetic: config-2 problems (createRandomVerticesPath + estimateSegmentTimes(2,2,6.5)) solved once; "
                 "candidates T_c = (0.5 + c/63) T")
     else:
@@ -272,10 +281,11 @@ def main():
         threads = int(os.environ.get("MTG_CPU_THREADS", min(16, os.cpu_count() or 1)))
         S = min(args.cpu_sample, B)
         if wl == "config5":
-            S = min(S, 2000)
+            S = min(S, 1000)
             rate, cel, done = cpu_baseline_cost(xfull[:S], times[:S], scales, N, r, args.cpu_seconds, threads)
             sample = ("%d trajectories x %d candidates of this rank's shard, evaluated repeatedly for %.1f s "
-                      "(%d candidate costs) by the oracle restatement (-O3 -march=native, OpenMP)"
+                      "(%d candidate cost+Jacobian evaluations; the Jacobian as the reference forms it, a "
+                      "central difference per segment) by the oracle restatement (-O3 -march=native, OpenMP)"
                       % (S, C5_CANDIDATES, cel, done))
         else:
             rate, cel, done = cpu_baseline(values[:S], mask[:S], times[:S], N, r, args.cpu_seconds, threads)

@@ -148,6 +148,25 @@ int mtg_cost_at_times_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to
                             const double* times, int n_candidates, const double* scales,
                             double* cost_out, double* grad_out, unsigned flags);
 
+/* Segment-time sweep of the fixed-derivative cost with its time Jacobian (BASELINE config 5, the
+ * matrix-core path).  Replaces, per trajectory b and candidate allocation c,
+ *   updateSegmentTimes(T_c) + getCostAndGradientDerivative(NULL)      nl_impl:1452-1520
+ * and the J_d part of getCostAndGradientTime's per-segment gradient    nl_impl:2153-2238
+ * (dJd_dt; the collision, soft-constraint and w_* weighting terms are not part of this path):
+ *   cost_out[b][c]      = sum_dims d^T R(T_c) d                 (as mtg_cost_at_times_batch)
+ *   jac_out[b][c][i]    = dJ/dT_i at T_c                        (nullable)
+ * with T_c[i] = times[b][i] * scales[c][i] and d = vertex_values[b] (ALL derivatives of every
+ * vertex, fixed and solved free ones).  increment_time == 0 gives the exact derivative;
+ * increment_time > 0 gives the reference's central difference
+ *   (J(T_i + dt) - J(T_i - dt)) / (2 dt), both perturbed times 0.1 when T_i <= 0.1
+ * (nl_impl:2180-2223; the reference default is increment_time = 0.1,
+ * polynomial_optimization_nonlinear.h:67); NaN where T_i - dt <= 0 (the reference CHECK-fails).
+ * Works for any n_candidates >= 1; per-call LDS limits the shape (MTG_ERR_TOO_LARGE). */
+int mtg_time_jacobian_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                            int64_t batch, const double* vertex_values, const double* times,
+                            int n_candidates, const double* scales, double increment_time,
+                            double* cost_out, double* jac_out, unsigned flags);
+
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -384,6 +385,63 @@ int mtg_cost_at_times_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to
   if (!dev) {
     MTG_HIP_TRY(ctx, hipMemcpyAsync(cost_out, base + o_cost, b_cost, hipMemcpyDeviceToHost, ctx->stream));
     if (grad_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(grad_out, base + o_grad, b_grad, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  } else if (!(flags & MTG_FLAG_ASYNC)) {
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return MTG_OK;
+}
+
+int mtg_time_jacobian_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
+                            int64_t batch, const double* vertex_values, const double* times,
+                            int n_candidates, const double* scales, double increment_time,
+                            double* cost_out, double* jac_out, unsigned flags) {
+  int rc = check_shape(ctx, N, D, K, derivative_to_optimize, batch);
+  if (rc != MTG_OK) return rc;
+  if (n_candidates < 1) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "n_candidates must be >= 1");
+  if (!(increment_time >= 0.0) || increment_time > DBL_MAX)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "increment_time must be finite and >= 0");
+  if (batch == 0) return MTG_OK;
+  if (!vertex_values || !times || !scales || !cost_out)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "vertex_values, times, scales, cost_out are required");
+  if (mtg::time_jacobian_lds_bytes(N, D, K, n_candidates) > 160 * 1024)
+    return set_error(ctx, MTG_ERR_TOO_LARGE, "per-block cost tables exceed LDS (reduce K or D)");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int V = K + 1, h = N / 2, C = n_candidates;
+  const size_t b_vals = sizeof(double) * (size_t)batch * V * h * D, b_times = sizeof(double) * (size_t)batch * K,
+               b_scales = sizeof(double) * (size_t)C * K, b_cost = sizeof(double) * (size_t)batch * C,
+               b_jac = jac_out ? sizeof(double) * (size_t)batch * C * K : 0;
+  const double *d_vals = vertex_values, *d_times = times, *d_scales = scales;
+  double *d_cost = cost_out, *d_jac = jac_out;
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  char* base = nullptr;
+  size_t o_cost = 0, o_jac = 0;
+  if (!dev) {
+    size_t off = 0;
+    const size_t o_vals = off; off = align_up(off + b_vals);
+    const size_t o_times = off; off = align_up(off + b_times);
+    const size_t o_scales = off; off = align_up(off + b_scales);
+    o_cost = off; off = align_up(off + b_cost);
+    o_jac = off; off = align_up(off + b_jac);
+    MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+    base = static_cast<char*>(ctx->staging);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_vals, vertex_values, b_vals, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_scales, scales, b_scales, hipMemcpyHostToDevice, ctx->stream));
+    d_vals = reinterpret_cast<const double*>(base + o_vals);
+    d_times = reinterpret_cast<const double*>(base + o_times);
+    d_scales = reinterpret_cast<const double*>(base + o_scales);
+    d_cost = reinterpret_cast<double*>(base + o_cost);
+    d_jac = jac_out ? reinterpret_cast<double*>(base + o_jac) : nullptr;
+  }
+  MTG_HIP_TRY(ctx, time_begin(ctx));
+  MTG_HIP_TRY(ctx, mtg::launch_time_jacobian(N, derivative_to_optimize, d_vals, d_times, d_scales, d_cost, d_jac,
+                                             increment_time, batch, K, D, C, ctx->stream));
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  if (!dev) {
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(cost_out, base + o_cost, b_cost, hipMemcpyDeviceToHost, ctx->stream));
+    if (jac_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(jac_out, base + o_jac, b_jac, hipMemcpyDeviceToHost, ctx->stream));
     MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   } else if (!(flags & MTG_FLAG_ASYNC)) {
     MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -45,6 +45,12 @@ hipError_t launch_cost_at_times(int N, int r, const double* values, const uint8_
                                 const double* scales, double* cost, double* grad, int64_t B, int K, int D, int C,
                                 hipStream_t stream);
 
+// segment-time cost sweep + time Jacobian on the matrix cores (mtg_jacobian.hip)
+size_t time_jacobian_lds_bytes(int N, int D, int K, int C);
+hipError_t launch_time_jacobian(int N, int r, const double* values, const double* times, const double* scales,
+                                double* cost, double* jac, double delta, int64_t B, int K, int D, int C,
+                                hipStream_t stream);
+
 // evaluateRange
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
                              double t_end, double dt, int64_t* counts, hipStream_t stream);

@@ -121,6 +121,24 @@ class Context:
                 nat.check(rc, handle)
         return call
 
+    def jacobian_call(self, N, r, vertex_values, times, scales, cost, jac, increment_time=0.0):
+        """Zero-argument callable: one asynchronous device-pointer mtg_time_jacobian_batch launch on
+        torch's current stream (the config-5 bench step: cost sweep + time Jacobian, matrix cores)."""
+        import torch
+        B, V, h, D = vertex_values.shape
+        C = scales.shape[0]
+        self.set_stream(torch.cuda.current_stream(vertex_values.device).cuda_stream)
+        fn = self._lib.mtg_time_jacobian_batch
+        args = (self.handle, N, D, V - 1, r, B, _addr(vertex_values), _addr(times), C, _addr(scales),
+                float(increment_time), _addr(cost), _addr(jac), nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC)
+        handle = self.handle
+
+        def call():
+            rc = fn(*args)
+            if rc:
+                nat.check(rc, handle)
+        return call
+
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
                            cost=None, status=None, split=False, asynchronous=False, general=False):
@@ -219,6 +237,25 @@ class Context:
                                                     _addr(times), C, _addr(scales), _addr(cost), _addr(g), 0),
                   self.handle)
         return (cost, g) if grad else cost
+
+    def time_jacobian_batch(self, N, r, vertex_values, times, scales, increment_time=0.0, jacobian=True):
+        """Cost sweep + segment-time Jacobian on the matrix cores (include/mtg.h mtg_time_jacobian_batch):
+        cost [B][C] = sum_dims d^T R(T_c) d and jac [B][C][K] = dJ/dT_i at T_c (exact for
+        increment_time == 0, the reference's central difference otherwise)."""
+        vertex_values = np.ascontiguousarray(vertex_values, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        scales = np.ascontiguousarray(scales, dtype=np.float64)
+        B, V, h, D = vertex_values.shape
+        K = V - 1
+        C = scales.shape[0]
+        assert scales.shape == (C, K) and times.shape == (B, K)
+        cost = np.empty((B, C))
+        jac = np.empty((B, C, K)) if jacobian else None
+        self.reset_stream()
+        nat.check(self._lib.mtg_time_jacobian_batch(self.handle, N, D, K, r, B, _addr(vertex_values), _addr(times),
+                                                    C, _addr(scales), float(increment_time), _addr(cost),
+                                                    _addr(jac), 0), self.handle)
+        return (cost, jac) if jacobian else cost
 
     # ------------------------------------------------------- evaluateRange
     def evaluate_range_batch(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True):

@@ -589,53 +589,119 @@ int64_t oracle_evaluate_range(int N, int D, int K, const double* coeffs, const d
 /* ------------------------------------------------------------------------ */
 /* Cost of fixed vertex derivatives at candidate times (config 5 CPU side)  */
 /* ------------------------------------------------------------------------ */
+/* Segment i's share of J_d = sum_dims x^T H(T) x, x = [d_i; d_{i+1}] (2h derivatives), with
+ * H = A^-T Q A^-1 formed as updateSegmentTimes (lin_impl:276-295) + constructR (:298-326) do. */
+static double segment_cost(int N, int D, int r, int nd, double T, const double* x, int i) {
+  const int h = N / 2;
+  double A[ORACLE_KMAXN * ORACLE_KMAXN], Ai[ORACLE_KMAXN * ORACLE_KMAXN], Q[ORACLE_KMAXN * ORACLE_KMAXN];
+  double T1[ORACLE_KMAXN * ORACLE_KMAXN], H[ORACLE_KMAXN * ORACLE_KMAXN];
+  oracle_setup_mapping_matrix(N, T, A);
+  oracle_invert_mapping_matrix(N, A, Ai);
+  oracle_quadratic_cost_jacobian(N, r, T, Q);
+  for (int p = 0; p < N; ++p)
+    for (int q = 0; q < N; ++q) {
+      double s = 0.0;
+      for (int k = 0; k < N; ++k) s += Q[p * N + k] * Ai[k * N + q];
+      T1[p * N + q] = s;
+    }
+  for (int p = 0; p < N; ++p)
+    for (int q = 0; q < N; ++q) {
+      double s = 0.0;
+      for (int k = 0; k < N; ++k) s += Ai[k * N + p] * T1[k * N + q];
+      H[p * N + q] = s;
+    }
+  double cost = 0.0;
+  for (int d = 0; d < D; ++d) {
+    double xs[ORACLE_KMAXN];
+    for (int k = 0; k < h; ++k) {
+      xs[k] = x[((size_t)i * nd + k) * D + d];
+      xs[h + k] = x[((size_t)(i + 1) * nd + k) * D + d];
+    }
+    for (int p = 0; p < N; ++p) {
+      double s = 0.0;
+      for (int q = 0; q < N; ++q) s += H[p * N + q] * xs[q];
+      cost += xs[p] * s;
+    }
+  }
+  return cost;
+}
+
 int oracle_cost_at_times_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
                                const double* times, int C, const double* scales, double* J,
                                int threads) {
   if (N < 2 || N > ORACLE_KMAXN || (N % 2) || K < 1 || D < 1 || C < 1 || nd < N / 2) return ORACLE_ERR_ARG;
-  const int h = N / 2, V = K + 1;
+  const int V = K + 1;
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 4)
 #endif
   for (int64_t b = 0; b < B; ++b) {
-    double A[ORACLE_KMAXN * ORACLE_KMAXN], Ai[ORACLE_KMAXN * ORACLE_KMAXN], Q[ORACLE_KMAXN * ORACLE_KMAXN];
-    double T1[ORACLE_KMAXN * ORACLE_KMAXN], H[ORACLE_KMAXN * ORACLE_KMAXN];
     const double* x = xfull + (size_t)b * V * nd * D;
     for (int c = 0; c < C; ++c) {
       double cost = 0.0;
-      for (int i = 0; i < K; ++i) {
-        const double T = times[(size_t)b * K + i] * scales[(size_t)c * K + i];
-        /* updateSegmentTimes: A, A^-1 (Schur), Q; then H = A^-T Q A^-1 as constructR forms it */
-        oracle_setup_mapping_matrix(N, T, A);
-        oracle_invert_mapping_matrix(N, A, Ai);
-        oracle_quadratic_cost_jacobian(N, r, T, Q);
-        for (int p = 0; p < N; ++p)
-          for (int q = 0; q < N; ++q) {
-            double s = 0.0;
-            for (int k = 0; k < N; ++k) s += Q[p * N + k] * Ai[k * N + q];
-            T1[p * N + q] = s;
-          }
-        for (int p = 0; p < N; ++p)
-          for (int q = 0; q < N; ++q) {
-            double s = 0.0;
-            for (int k = 0; k < N; ++k) s += Ai[k * N + p] * T1[k * N + q];
-            H[p * N + q] = s;
-          }
-        for (int d = 0; d < D; ++d) {
-          double xs[ORACLE_KMAXN];
-          for (int k = 0; k < h; ++k) {
-            xs[k] = x[((size_t)i * nd + k) * D + d];
-            xs[h + k] = x[((size_t)(i + 1) * nd + k) * D + d];
-          }
-          for (int p = 0; p < N; ++p) {
-            double s = 0.0;
-            for (int q = 0; q < N; ++q) s += H[p * N + q] * xs[q];
-            cost += xs[p] * s;
-          }
-        }
-      }
+      for (int i = 0; i < K; ++i)
+        cost += segment_cost(N, D, r, nd, times[(size_t)b * K + i] * scales[(size_t)c * K + i], x, i);
       J[(size_t)b * C + c] = cost;
+    }
+  }
+  (void)threads;
+  return ORACLE_OK;
+}
+
+/* getCostAndGradientTime's J_d gradient (polynomial_optimization_nonlinear_impl.h:2172-2229):
+ * for each segment n, updateSegmentTimes with T_n -+ increment_time (both 0.1 when T_n <= 0.1,
+ * :2182, :2201), getCostAndGradientDerivative at each, central difference.  The full J_d sums are
+ * recomputed as the reference does.  increment_time == 0 asks for the exact derivative: the limit
+ * of the same central difference, taken by Richardson extrapolation over steps 2e-2 T_n / 2^k on
+ * segment n's share (the other segments' shares cancel exactly in the difference). */
+int oracle_cost_time_jacobian_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
+                                    const double* times, int C, const double* scales, double increment_time,
+                                    double* J, double* G, int threads) {
+  if (N < 2 || N > ORACLE_KMAXN || (N % 2) || K < 1 || D < 1 || C < 1 || nd < N / 2 || K > 256 ||
+      !(increment_time >= 0.0))
+    return ORACLE_ERR_ARG;
+  const int V = K + 1;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t b = 0; b < B; ++b) {
+    const double* x = xfull + (size_t)b * V * nd * D;
+    double Tc[256], share[256];
+    for (int c = 0; c < C; ++c) {
+      double tot = 0.0;
+      for (int i = 0; i < K; ++i) {
+        Tc[i] = times[(size_t)b * K + i] * scales[(size_t)c * K + i];
+        share[i] = segment_cost(N, D, r, nd, Tc[i], x, i);
+        tot += share[i];
+      }
+      J[(size_t)b * C + c] = tot;
+      if (!G) continue;
+      for (int n = 0; n < K; ++n) {
+        double g;
+        if (increment_time > 0.0) {
+          const double dt = increment_time;
+          const double tm = Tc[n] <= 0.1 ? 0.1 : Tc[n] - dt, tp = Tc[n] <= 0.1 ? 0.1 : Tc[n] + dt;
+          double jm = 0.0, jp = 0.0;
+          for (int i = 0; i < K; ++i) {
+            jm += i == n ? segment_cost(N, D, r, nd, tm, x, i) : share[i];
+            jp += i == n ? segment_cost(N, D, r, nd, tp, x, i) : share[i];
+          }
+          g = (jp - jm) / (2.0 * dt);
+        } else {
+          double R[4][4];
+          double hs = 2e-2 * Tc[n];
+          for (int k = 0; k < 4; ++k, hs *= 0.5)
+            R[k][0] = (segment_cost(N, D, r, nd, Tc[n] + hs, x, n) - segment_cost(N, D, r, nd, Tc[n] - hs, x, n)) /
+                      (2.0 * hs);
+          for (int j = 1; j < 4; ++j) {
+            const double f = pow(4.0, j);
+            for (int k = j; k < 4; ++k) R[k][j] = (f * R[k][j - 1] - R[k - 1][j - 1]) / (f - 1.0);
+          }
+          g = R[3][3];
+        }
+        G[((size_t)b * C + c) * K + n] = g;
+      }
     }
   }
   (void)threads;

@@ -105,6 +105,12 @@ void oracle_quadratic_cost_jacobian(int N, int derivative, double T, double* Q);
 int oracle_cost_at_times_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
                                const double* times, int C, const double* scales, double* J,
                                int threads);
+/* getCostAndGradientTime's J_d term (polynomial_optimization_nonlinear_impl.h:2172-2229) at the
+ * same candidates: G[b][c][n] = central difference of J_d in T_n with increment_time (the
+ * reference's 0.1 floor included), or the exact derivative (Richardson limit) for 0. */
+int oracle_cost_time_jacobian_batch(int N, int D, int K, int r, int nd, int64_t B, const double* xfull,
+                                    const double* times, int C, const double* scales, double increment_time,
+                                    double* J, double* G, int threads);
 
 /* Batched convenience for the CPU baseline: B problems with identical shape,
  * values [B][V][nd][D] etc.  Runs on `threads` OpenMP threads (<=0: all). */

@@ -83,6 +83,9 @@ def lib(path=None):
     L.oracle_evaluate_range.restype = ctypes.c_int64
     L.oracle_cost_at_times_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int64, _dp, _dp, ctypes.c_int, _dp, _dp, ctypes.c_int]
+    L.oracle_cost_time_jacobian_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_int, ctypes.c_int64, _dp, _dp, ctypes.c_int, _dp,
+                                                  ctypes.c_double, _dp, _dp, ctypes.c_int]
     if path is None or _LIB is None:
         _LIB = L
     return L
@@ -244,3 +247,19 @@ def cost_at_times_batch(N, r, xfull, times, scales, threads=0):
     rc = lib().oracle_cost_at_times_batch(N, D, V - 1, r, nd, B, _p(xfull), _p(times), C, _p(scales), _p(J), threads)
     assert rc == 0, rc
     return J
+
+
+def cost_time_jacobian_batch(N, r, xfull, times, scales, increment_time=0.0, threads=0):
+    """getCostAndGradientTime's J_d gradient at candidate times (oracle_cost_time_jacobian_batch).
+    xfull [B][V][nd][D], times [B][K], scales [C][K] -> (J [B][C], G [B][C][K])."""
+    xfull = np.ascontiguousarray(xfull, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    scales = np.ascontiguousarray(scales, dtype=np.float64)
+    B, V, nd, D = xfull.shape
+    C = scales.shape[0]
+    J = np.empty((B, C))
+    G = np.empty((B, C, V - 1))
+    rc = lib().oracle_cost_time_jacobian_batch(N, D, V - 1, r, nd, B, _p(xfull), _p(times), C, _p(scales),
+                                               float(increment_time), _p(J), _p(G), threads)
+    assert rc == 0, rc
+    return J, G

@@ -44,6 +44,7 @@ def counter_means(path, skip_first=2):
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     return name.split("(")[0].replace("void ", "").replace("mtg::", "").split("<")[0]
 
 

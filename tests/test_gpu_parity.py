@@ -287,3 +287,64 @@ def test_cost_at_times_vs_oracle(gpu_ctx):
     # optimality at the solved times: 2 (R d)_free = 0 up to rounding
     g1 = np.abs(g[:, 1]).max(axis=(1, 2))
     assert np.all(np.abs(g[:, 0]).max(axis=(1, 2)) <= 1e-6 * g1)
+
+
+def _solved_full_values(gpu_ctx, N, r, vals, mask, times):
+    from mav_trajectory_generation_cmake_amd import full_vertex_values
+    sol = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, free=True, cost=True)
+    return full_vertex_values(vals, mask, sol["free"], N), sol
+
+
+@pytest.mark.parametrize("C", [64, 20])
+def test_time_jacobian_vs_oracle(gpu_ctx, C):
+    """Config 5 on the matrix cores (mtg_time_jacobian_batch): cost sweep J(T_c) and the exact
+    segment-time Jacobian against the oracle (reference H = A^-T Q A^-1 per segment; Richardson limit
+    of getCostAndGradientTime's central difference).  B = 37 and C = 20 exercise the ragged row and
+    column tiles."""
+    O = _oracle()
+    N, r, K, B = 10, 4, 10, 37
+    vals, mask, times = _bench_batch(B, seed0=310, K=K)
+    xf, sol = _solved_full_values(gpu_ctx, N, r, vals, mask, times)
+    rng = np.random.default_rng(3)
+    scales = np.repeat((0.5 + np.arange(C) / max(C - 1, 1))[:, None], K, axis=1)
+    scales[1::2] *= rng.uniform(0.8, 1.2, size=(C // 2, K))
+    scales[0] = 1.0
+    J, G = gpu_ctx.time_jacobian_batch(N, r, xf, times, scales)
+    np.testing.assert_allclose(J[:, 0], 2.0 * sol["cost"], rtol=1e-9)
+    Jc = gpu_ctx.cost_at_times_batch(N, r, xf, times, scales)  # the VALU kernel: same numbers
+    np.testing.assert_allclose(J, Jc, rtol=1e-11)
+    sel = [0, 1, 16, 36]
+    Jr, Gr = O.cost_time_jacobian_batch(N, r, xf[sel], times[sel], scales, 0.0)
+    np.testing.assert_allclose(J[sel], Jr, rtol=1e-7)
+    gscale = np.max(np.abs(Gr), axis=2, keepdims=True)
+    assert np.max(np.abs(G[sel] - Gr) / gscale) <= 1e-6
+
+
+def test_time_jacobian_reference_difference(gpu_ctx):
+    """increment_time > 0: the reference's central difference (nl_impl:2180-2223) on N=12 / K=20 /
+    JERK shapes (config 4 generator), and its 0.1 floor: a segment at or below 0.1 s gets exactly 0."""
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch
+    O = _oracle()
+    N, r, K, B, C = 12, 3, 20, 18, 5
+    vals, mask, times = random_vertices_batch(N, 3, K, B, [-10, -20, -10], [10, 20, 10], seed0=77)
+    xf, _ = _solved_full_values(gpu_ctx, N, r, vals, mask, times)
+    scales = np.ones((C, K))
+    scales[1:] = np.random.default_rng(5).uniform(0.8, 1.2, size=(C - 1, K))
+    dt = 0.1
+    J, G = gpu_ctx.time_jacobian_batch(N, r, xf, times, scales, increment_time=dt)
+    Jr, Gr = O.cost_time_jacobian_batch(N, r, xf, times, scales, dt)
+    # N=12: the reference's FP64 A^-1 / H path is itself ~1e-6 from truth (SURVEY.md App. A)
+    np.testing.assert_allclose(J, Jr, rtol=1e-6)
+    # the reference differences two full sums, each carrying that error: ~1e-6 |J| / dt
+    tol = 2e-6 * np.abs(Jr)[..., None] / dt + 1e-7 * np.max(np.abs(Gr), axis=2, keepdims=True)
+    assert np.all(np.abs(G - Gr) <= tol)
+    # the floor (config-2 shape): both perturbed times become 0.1, the difference is exactly 0
+    N, r, K = 10, 4, 10
+    vals, mask, times = _bench_batch(3, seed0=90, K=K)
+    times[0, 4] = 0.08
+    times[1, 2] = 0.1
+    xf, _ = _solved_full_values(gpu_ctx, N, r, vals, mask, times)
+    J, G = gpu_ctx.time_jacobian_batch(N, r, xf, times, np.ones((1, K)), increment_time=dt)
+    _, Gr = O.cost_time_jacobian_batch(N, r, xf, times, np.ones((1, K)), dt)
+    assert G[0, 0, 4] == 0.0 and G[1, 0, 2] == 0.0 and Gr[0, 0, 4] == 0.0 and Gr[1, 0, 2] == 0.0
+    assert np.count_nonzero(G == 0.0) == 2 and np.isfinite(J).all()

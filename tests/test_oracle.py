@@ -241,3 +241,71 @@ def test_cost_at_times_oracle_consistency():
     J = O.cost_at_times_batch(10, 4, xf, times, np.array([[1.0] * 10, [2.0] * 10]))
     np.testing.assert_allclose(J[:, 0], 2 * cost, rtol=1e-9)
     assert np.all(J[:, 1] > 0) and np.all(np.isfinite(J[:, 1]))
+
+
+def _mp_segment_cost(N, r, T, xs):
+    """sum_dims x^T A^-T Q A^-1 x for one segment in 40-digit arithmetic (independent of the
+    oracle: exact A(T) of lin_impl:102-111 and Q(T) of :574-589, mpmath inverse)."""
+    import mpmath as mp
+    h = N // 2
+    T = mp.mpf(T)
+
+    def ff(i, n):  # falling factorial i!/(i-n)!
+        return mp.mpf(0) if i < n else mp.factorial(i) / mp.factorial(i - n)
+    A = mp.matrix(N, N)
+    for d in range(h):
+        for j in range(N):
+            A[d, j] = ff(j, d) * (mp.mpf(0) ** (j - d) if j >= d else 0) if j != d else ff(j, d)
+            A[h + d, j] = ff(j, d) * T ** (j - d) if j >= d else 0
+    Q = mp.matrix(N, N)
+    for i in range(r, N):
+        for j in range(r, N):
+            e = i + j - 2 * r + 1
+            Q[i, j] = 2 * ff(i, r) * ff(j, r) * T ** e / e
+    Ai = A ** -1
+    H = Ai.T * Q * Ai
+    tot = mp.mpf(0)
+    for x in xs:
+        v = mp.matrix([mp.mpf(float(t)) for t in x])
+        tot += (v.T * H * v)[0]
+    return tot
+
+
+def test_time_jacobian_oracle_vs_mpmath():
+    """The oracle's exact time derivative of J_d (Richardson limit of the reference's central
+    difference) against mpmath.diff of the independently built 40-digit segment cost; the
+    increment_time mode equals the reference's formula applied to oracle_cost_at_times_batch."""
+    import mpmath as mp
+    with mp.workdps(40):
+        _time_jacobian_checks(mp)
+
+
+def _time_jacobian_checks(mp):
+    rng = np.random.default_rng(7)
+    N, r, K, D = 6, 2, 3, 2
+    h = N // 2
+    xf = rng.uniform(-3, 3, size=(1, K + 1, h, D))
+    times = np.array([[0.7, 1.9, 0.35]])
+    scales = np.array([[1.0, 1.0, 1.0], [1.3, 0.8, 1.1]])
+    J, G = O.cost_time_jacobian_batch(N, r, xf, times, scales, 0.0)
+    for c in range(2):
+        Jm = 0.0
+        for n in range(K):
+            Tn = times[0, n] * scales[c, n]
+            xs = [np.concatenate([xf[0, n, :, d], xf[0, n + 1, :, d]]) for d in range(D)]
+            Jm += float(_mp_segment_cost(N, r, Tn, xs))
+            gm = float(mp.diff(lambda t: _mp_segment_cost(N, r, t, xs), mp.mpf(Tn)))
+            assert abs(G[0, c, n] - gm) <= 1e-8 * abs(gm), (c, n, G[0, c, n], gm)
+        assert abs(J[0, c] - Jm) <= 1e-11 * abs(Jm)
+    # increment_time mode: (J(T_n + dt) - J(T_n - dt)) / (2 dt) with the 0.1 floor
+    dt = 0.1
+    times2 = np.array([[0.7, 0.08, 0.35]])  # segment 1 is below the floor: gradient 0
+    J2, G2 = O.cost_time_jacobian_batch(N, r, xf, times2, scales[:1], dt)
+    for n in range(K):
+        sp = np.ones((2, K))
+        sp[0, n] = (times2[0, n] + dt) / times2[0, n]
+        sp[1, n] = (times2[0, n] - dt) / times2[0, n]
+        Jpm = O.cost_at_times_batch(N, r, xf, times2, sp)
+        want = 0.0 if times2[0, n] <= 0.1 else (Jpm[0, 0] - Jpm[0, 1]) / (2 * dt)
+        assert abs(G2[0, 0, n] - want) <= 1e-9 * max(abs(J2[0, 0]), 1.0) / dt, (n, G2[0, 0, n], want)
+    assert G2[0, 0, 1] == 0.0
