@@ -18,6 +18,7 @@ ctx = mtg.Context(0)
 for _ in range(3):
     out = ctx.solve_linear_batch(10, 4, vals, mask, times, free=True)
 f = out["free"].reshape(B, -1)[:, :4]
+sub = out["free"].reshape(B, -1)[:, 4:9]
 names = ["staging", "forward", "backward", "epilogue"]
 tot = f.sum(axis=1)
 print("B=%d cycles per wave (mean over trajectories; s_memtime ticks)" % B)
@@ -26,3 +27,8 @@ for i, n in enumerate(names):
                                                              np.percentile(f[:, i], 90),
                                                              100 * f[:, i].mean() / tot.mean()))
 print("  total     mean %8.0f" % tot.mean())
+names = ["products", "exchange", "factor+solve"]
+print("  forward sub-phases (sum over vertices; s_memtime waits for LDS at each mark):")
+for i, n in enumerate(names):
+    print("    %-13s mean %8.0f" % (n, sub[:, i].mean()))
+print("  epilogue: A(1)^-1 table load %8.0f   coefficient stores (issue) %8.0f" % (sub[:, 3].mean(), sub[:, 4].mean()))
