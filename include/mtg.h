@@ -167,6 +167,22 @@ int mtg_time_jacobian_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to
                             int n_candidates, const double* scales, double increment_time,
                             double* cost_out, double* jac_out, unsigned flags);
 
+/* Coefficients from ALL vertex derivatives (fixed and free), nothing solved: per trajectory the
+ * reference's setFreeConstraints (polynomial_optimization_linear.h:185-186) followed by
+ * updateSegmentsFromCompactConstraints (lin_impl:253-273), c_i = A(T_i)^-1 [x_i; x_{i+1}].
+ * vertex_values [B][V][h][D], times [B][K] (> 0) -> coeffs [B][K][D][N]. */
+int mtg_coefficients_from_vertices_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
+                                         const double* vertex_values, const double* times, double* coeffs,
+                                         unsigned flags);
+
+/* Vertex derivatives of solved trajectories: the reference's M^+ A p
+ * (polynomial_optimization_nonlinear_impl.h:162-180, computeInitialSolutionWithoutPositionConstraints;
+ * getA / getMpinv, polynomial_optimization_linear.h:209-214): derivative k < h of every segment end,
+ * averaged over the two segment ends meeting at an interior vertex.
+ * coeffs [B][K][D][N], times [B][K] -> vertex_values [B][V][h][D]. */
+int mtg_vertex_derivatives_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                 const double* times, double* vertex_values, unsigned flags);
+
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);

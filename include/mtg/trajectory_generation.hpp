@@ -336,6 +336,53 @@ class PolynomialOptimization {
     for (int d = 0; d < D_; ++d)
       for (int i = 0; i < n_free_; ++i) (*free_constraints)[d][i] = free_[(size_t)d * V * h + i];
   }
+  // getFixedConstraints (polynomial_optimization_linear.h:188-192): per dimension, fixed
+  // derivatives in (vertex, derivative) order
+  void getFixedConstraints(std::vector<std::vector<double>>* fixed_constraints) const {
+    const int V = K_ + 1, h = N / 2;
+    fixed_constraints->assign(D_, std::vector<double>());
+    for (int v = 0; v < V; ++v)
+      for (int k = 0; k < h; ++k)
+        if ((mask_[v] >> k) & 1u)
+          for (int d = 0; d < D_; ++d) (*fixed_constraints)[d].push_back(values_[((size_t)v * h + k) * D_ + d]);
+  }
+  // setFreeConstraints (polynomial_optimization_linear.h:185-186) + updateSegmentsFromCompactConstraints
+  // (lin_impl:253-273): new free derivatives (per dimension, reference order), coefficients recomputed
+  // on the GPU (mtg_coefficients_from_vertices_batch); computeCost() follows the new coefficients.
+  void setFreeConstraints(const std::vector<std::vector<double>>& free_constraints) {
+    const int V = K_ + 1, h = N / 2;
+    if ((int)free_constraints.size() != D_) fail(MTG_ERR_SIZE_MISMATCH, "setFreeConstraints: dimension mismatch");
+    const int nf = (int)(V * h - getNumberFixedConstraints());
+    std::vector<double> x((size_t)V * h * D_, 0.0);
+    free_.assign((size_t)D_ * V * h, 0.0);
+    for (int d = 0; d < D_; ++d) {
+      if ((int)free_constraints[d].size() != nf) fail(MTG_ERR_SIZE_MISMATCH, "setFreeConstraints: size mismatch");
+      int idx = 0;
+      for (int v = 0; v < V; ++v)
+        for (int k = 0; k < h; ++k) {
+          const size_t o = ((size_t)v * h + k) * D_ + d;
+          if ((mask_[v] >> k) & 1u) {
+            x[o] = values_[o];
+          } else {
+            x[o] = free_constraints[d][idx];
+            free_[(size_t)d * V * h + idx] = free_constraints[d][idx];
+            ++idx;
+          }
+        }
+    }
+    n_free_ = nf;
+    mtg_ctx* ctx = default_context();
+    coeffs_.assign((size_t)K_ * D_ * N, 0.0);
+    check(mtg_coefficients_from_vertices_batch(ctx, N, D_, K_, 1, x.data(), times_.data(), coeffs_.data(), 0), ctx,
+          "mtg_coefficients_from_vertices_batch");
+    std::vector<double> scales(K_, 1.0);
+    double J = 0.0;
+    check(mtg_cost_at_times_batch(ctx, N, D_, K_, r_, 1, x.data(), nullptr, times_.data(), 1, scales.data(), &J,
+                                  nullptr, 0),
+          ctx, "mtg_cost_at_times_batch");
+    cost_ = 0.5 * J;  // computeCost = 0.5 sum c^T Q c; J = d^T R d (nl_impl:1499-1502)
+    solved_ = true;
+  }
   size_t getNumberFreeConstraints() const { return n_free_; }
   size_t getNumberFixedConstraints() const {
     size_t n = 0;
@@ -355,6 +402,41 @@ class PolynomialOptimization {
   int n_free_ = 0;
   double cost_ = 0.0;
 };
+
+// PolynomialOptimizationNonLinear::computeInitialSolutionWithoutPositionConstraints
+// (polynomial_optimization_nonlinear_impl.h:116-187) on a linear problem: solve, remove the position
+// constraint of every interior vertex, set the problem up again with the same times and start its
+// free derivatives from the solved trajectory (M^+ A p, mtg_vertex_derivatives_batch).  The
+// polynomials are unchanged up to rounding; the free vector now holds the interior positions too.
+template <int N>
+bool computeInitialSolutionWithoutPositionConstraints(PolynomialOptimization<N>* opt) {
+  opt->solveLinear();
+  Segment::Vector segments;
+  opt->getSegments(&segments);
+  std::vector<double> times;
+  opt->getSegmentTimes(&times);
+  Vertex::Vector vertices;
+  opt->getVertices(&vertices);
+  const int K = (int)times.size(), D = opt->getDimension(), h = N / 2, V = K + 1;
+  std::vector<double> coeffs((size_t)K * D * N), x((size_t)V * h * D);
+  for (int i = 0; i < K; ++i)
+    for (int d = 0; d < D; ++d) {
+      const auto& c = segments[i][d].getCoefficients();
+      for (int j = 0; j < N; ++j) coeffs[((size_t)i * D + d) * N + j] = c[j];
+    }
+  mtg_ctx* ctx = default_context();
+  check(mtg_vertex_derivatives_batch(ctx, N, D, K, 1, coeffs.data(), times.data(), x.data(), 0), ctx,
+        "mtg_vertex_derivatives_batch");
+  for (int v = 1; v < V - 1; ++v) vertices[v].removeConstraint(derivative_order::POSITION);
+  opt->setupFromVertices(vertices, times, opt->getDerivativeToOptimize());
+  std::vector<std::vector<double>> free(D);
+  for (int v = 0; v < V; ++v)
+    for (int k = 0; k < h; ++k)
+      if (!vertices[v].hasConstraint(k))
+        for (int d = 0; d < D; ++d) free[d].push_back(x[((size_t)v * h + k) * D + d]);
+  opt->setFreeConstraints(free);
+  return true;
+}
 
 // ------------------------------------------------------------- BatchPolynomialOptimization<N>
 // B independent problems of one shape (N, D, K, r) per call: the throughput API.  Arrays are in
@@ -382,6 +464,24 @@ class BatchPolynomialOptimization {
     check(mtg_time_sweep_batch(ctx_, N, D_, K_, r_, batch, values, mask, times, n_candidates, scales, cost, status,
                                flags),
           ctx_, "mtg_time_sweep_batch");
+  }
+  // config 5: cost sweep + segment-time Jacobian on the matrix cores (mtg_time_jacobian_batch)
+  void timeJacobian(int64_t batch, const double* vertex_values, const double* times, int n_candidates,
+                    const double* scales, double* cost, double* jac, double increment_time = 0.0,
+                    unsigned flags = 0) {
+    check(mtg_time_jacobian_batch(ctx_, N, D_, K_, r_, batch, vertex_values, times, n_candidates, scales,
+                                  increment_time, cost, jac, flags),
+          ctx_, "mtg_time_jacobian_batch");
+  }
+  void coefficientsFromVertices(int64_t batch, const double* vertex_values, const double* times, double* coeffs,
+                                unsigned flags = 0) {
+    check(mtg_coefficients_from_vertices_batch(ctx_, N, D_, K_, batch, vertex_values, times, coeffs, flags), ctx_,
+          "mtg_coefficients_from_vertices_batch");
+  }
+  void vertexDerivatives(int64_t batch, const double* coeffs, const double* times, double* vertex_values,
+                         unsigned flags = 0) {
+    check(mtg_vertex_derivatives_batch(ctx_, N, D_, K_, batch, coeffs, times, vertex_values, flags), ctx_,
+          "mtg_vertex_derivatives_batch");
   }
   mtg_ctx* context() const { return ctx_; }
 

@@ -61,6 +61,10 @@ _SIGNATURES = {
     "mtg_time_jacobian_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int, _c_dp,
                                                ctypes.c_double, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_coefficients_from_vertices_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                            ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_vertex_derivatives_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
     "mtg_last_kernel_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "mtg_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mtg_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,

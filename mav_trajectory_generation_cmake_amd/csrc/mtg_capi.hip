@@ -449,6 +449,67 @@ int mtg_time_jacobian_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to
   return MTG_OK;
 }
 
+namespace {
+
+// Shared body of the two vertex <-> coefficient maps: [B][V][h][D] <-> [B][K][D][N].
+int run_vertex_map(mtg_ctx* ctx, bool to_coeffs, int N, int D, int K, int64_t batch, const double* in,
+                   const double* times, double* out, unsigned flags) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  if (N < 2 || N > 12 || (N % 2)) return set_error(ctx, MTG_ERR_UNSUPPORTED_N, "N must be even and in [2, 12]");
+  if (K < 1 || D < 1 || batch < 0) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "need K >= 1, D >= 1, batch >= 0");
+  if (!mtg::vertex_map_fits(N, D, K))
+    return set_error(ctx, MTG_ERR_TOO_LARGE, "per-trajectory arrays exceed the LDS staging (reduce K or D)");
+  if (batch == 0) return MTG_OK;
+  if (!in || !times || !out) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "input, times and output are required");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int V = K + 1, h = N / 2;
+  const size_t b_vals = sizeof(double) * (size_t)batch * V * h * D, b_coef = sizeof(double) * (size_t)batch * K * D * N,
+               b_times = sizeof(double) * (size_t)batch * K;
+  const size_t b_in = to_coeffs ? b_vals : b_coef, b_out = to_coeffs ? b_coef : b_vals;
+  const double *d_in = in, *d_times = times;
+  double* d_out = out;
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  char* base = nullptr;
+  size_t o_out = 0;
+  if (!dev) {
+    size_t off = 0;
+    const size_t o_in = off; off = align_up(off + b_in);
+    const size_t o_times = off; off = align_up(off + b_times);
+    o_out = off; off = align_up(off + b_out);
+    MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+    base = static_cast<char*>(ctx->staging);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_in, in, b_in, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+    d_in = reinterpret_cast<const double*>(base + o_in);
+    d_times = reinterpret_cast<const double*>(base + o_times);
+    d_out = reinterpret_cast<double*>(base + o_out);
+  }
+  MTG_HIP_TRY(ctx, time_begin(ctx));
+  MTG_HIP_TRY(ctx, mtg::launch_vertex_map(to_coeffs, N, d_in, d_times, d_out, batch, K, D, ctx->stream));
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  if (!dev) {
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(out, base + o_out, b_out, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  } else if (!(flags & MTG_FLAG_ASYNC)) {
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return MTG_OK;
+}
+
+}  // namespace
+
+int mtg_coefficients_from_vertices_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
+                                         const double* vertex_values, const double* times, double* coeffs,
+                                         unsigned flags) {
+  return run_vertex_map(ctx, true, N, D, K, batch, vertex_values, times, coeffs, flags);
+}
+
+int mtg_vertex_derivatives_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                 const double* times, double* vertex_values, unsigned flags) {
+  return run_vertex_map(ctx, false, N, D, K, batch, coeffs, times, vertex_values, flags);
+}
+
 int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
                              const double* coeffs, const double* times, double t_start,
                              double t_end, double dt, int derivative, int64_t* counts,

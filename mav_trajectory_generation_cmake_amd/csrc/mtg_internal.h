@@ -51,6 +51,11 @@ hipError_t launch_time_jacobian(int N, int r, const double* values, const double
                                 double* cost, double* jac, double delta, int64_t B, int K, int D, int C,
                                 hipStream_t stream);
 
+// vertex derivatives <-> coefficients (mtg_vertex.hip)
+bool vertex_map_fits(int N, int D, int K);
+hipError_t launch_vertex_map(bool to_coeffs, int N, const double* in, const double* times, double* out, int64_t B,
+                             int K, int D, hipStream_t stream);
+
 // evaluateRange
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
                              double t_end, double dt, int64_t* counts, hipStream_t stream);

@@ -247,8 +247,16 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
 
   // ---- epilogue: coefficients c = diag(T^-j) A(1)^-1 S(T) [x_i; x_{i+1}] and the cost, items (i, d)
   double cacc = 0.0;
-  for (int it = c; it < K * D; it += LG) {
-    const int i = it / D, dd = it - i * D;
+  // Items (segment i, dimension dd) go in rounds of LG, item it = base + c.  A round's coefficient
+  // rows are consecutive in HBM ([K][D][N] per trajectory): when the G store (dead after the
+  // backward sweep) can hold them they are staged there and stored as one contiguous run per
+  // trajectory, 16 B per lane at consecutive addresses (per-lane 16-B pieces at an N-double
+  // stride kept the store unit busy for most of the epilogue; see mtg_solve_reg.inc).
+  const bool stage = K * H * H >= LG * N && !(slot_doubles(H, D, K, LG) & 1);  // room, 16-B aligned
+  for (int base = 0; base < K * D; base += LG) {
+    const int it = base + c;
+    const bool have = it < K * D;
+    const int i = have ? it / D : 0, dd = have ? it - i * D : 0;
     cdouble* Hl = launder(c_htilde + MTG_HTILDE_OFF(N, R));
     cdouble* Ai1 = launder(c_a1inv + MTG_A1INV_OFF(N));
     const double T = tms[i] * tscale;
@@ -285,13 +293,25 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
         out[j] = acc * tp;
         tp *= tinv;
       }
-      if (valid) {
+      if (stage) {
+        double2* o2 = reinterpret_cast<double2*>(gst + c * N);
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) o2[j] = make_double2(out[2 * j], out[2 * j + 1]);
+        __syncthreads();  // (one wave per block: orders the LDS staging)
+        const int nrun = (K * D - base < LG ? K * D - base : LG) * (N / 2);  // double2s this round
+        if (valid) {
+          double2* dst = reinterpret_cast<double2*>(a.coeffs + (pb * (K * D) + base) * N);
+          const double2* src = reinterpret_cast<const double2*>(gst);
+          for (int e = c; e < nrun; e += LG) dst[e] = src[e];
+        }
+        __syncthreads();
+      } else if (valid && have) {
         double2* dst = reinterpret_cast<double2*>(a.coeffs + ((pb * K + i) * D + dd) * N);
 #pragma unroll
         for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(out[2 * j], out[2 * j + 1]);
       }
     }
-    if (a.cost_out) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)
+    if (a.cost_out && have) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)
       if (R == 0) sh[0] = p0, sh[H] += p0;
       double q = 0.0;
 #pragma unroll

@@ -257,6 +257,60 @@ class Context:
                                                     _addr(jac), 0), self.handle)
         return (cost, jac) if jacobian else cost
 
+    def coefficients_from_vertices_batch(self, N, vertex_values, times):
+        """setFreeConstraints + updateSegmentsFromCompactConstraints (include/mtg.h
+        mtg_coefficients_from_vertices_batch): [B][V][h][D] all vertex derivatives -> [B][K][D][N]."""
+        vertex_values = np.ascontiguousarray(vertex_values, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        B, V, h, D = vertex_values.shape
+        K = V - 1
+        assert h == N // 2 and times.shape == (B, K)
+        out = np.empty((B, K, D, N))
+        self.reset_stream()
+        nat.check(self._lib.mtg_coefficients_from_vertices_batch(self.handle, N, D, K, B, _addr(vertex_values),
+                                                                 _addr(times), _addr(out), 0), self.handle)
+        return out
+
+    def vertex_derivatives_batch(self, coeffs, times):
+        """M^+ A p (include/mtg.h mtg_vertex_derivatives_batch): [B][K][D][N] -> [B][V][h][D]."""
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        B, K, D, N = coeffs.shape
+        assert times.shape == (B, K)
+        out = np.empty((B, K + 1, N // 2, D))
+        self.reset_stream()
+        nat.check(self._lib.mtg_vertex_derivatives_batch(self.handle, N, D, K, B, _addr(coeffs), _addr(times),
+                                                         _addr(out), 0), self.handle)
+        return out
+
+    def set_free_constraints_batch(self, N, values, mask, times, free):
+        """PolynomialOptimization::setFreeConstraints (polynomial_optimization_linear.h:185-186) for a
+        batch: the fixed values stay, the free derivatives come from `free` [B][D][V*h] (reference
+        order); returns the recomputed coefficients [B][K][D][N] (lin_impl:253-273)."""
+        return self.coefficients_from_vertices_batch(N, full_vertex_values(values, mask, free, N), times)
+
+    def initial_solution_without_position_constraints(self, N, r, values, mask, times):
+        """PolynomialOptimizationNonLinear::computeInitialSolutionWithoutPositionConstraints
+        (polynomial_optimization_nonlinear_impl.h:116-187) for a batch: solve, drop every position
+        constraint except at the first and last vertex, and start the new free derivatives from the
+        solved trajectory (M^+ A p).  Returns dict(mask, values, free [B][D][V*h], n_free, coeffs):
+        the new problem (mask, values) and its free-constraint vector; re-solving it reproduces the
+        same trajectory up to rounding."""
+        values = np.ascontiguousarray(values, dtype=np.float64)
+        B, V, h, D = values.shape
+        sol = self.solve_linear_batch(N, r, values, mask, times)
+        allv = self.vertex_derivatives_batch(sol["coeffs"], times)
+        new_mask = np.array(mask, dtype=np.uint8, copy=True)
+        new_mask[:, 1:V - 1] &= np.uint8(0xFE)  # vertices_[k].removeConstraint(POSITION), 0 < k < V-1
+        fixed = ((new_mask[:, :, None] >> np.arange(h)[None, None, :]) & 1).astype(bool)  # [B][V][h]
+        free = np.zeros((B, D, V * h))
+        n_free = np.zeros(B, dtype=np.int32)
+        for b in range(B):
+            slots = np.flatnonzero(~fixed[b].reshape(-1))  # reference (vertex, derivative) order
+            n_free[b] = len(slots)
+            free[b, :, :len(slots)] = allv[b].reshape(-1, D)[slots].T
+        return {"mask": new_mask, "values": values, "free": free, "n_free": n_free, "coeffs": sol["coeffs"]}
+
     # ------------------------------------------------------- evaluateRange
     def evaluate_range_batch(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True):
         """Host-array convenience wrapper: returns (samples [S][D], sample_times [S], counts [B], offsets [B])."""

@@ -263,3 +263,38 @@ def cost_time_jacobian_batch(N, r, xfull, times, scales, increment_time=0.0, thr
                                                float(increment_time), _p(J), _p(G), threads)
     assert rc == 0, rc
     return J, G
+
+
+def vertex_derivatives(N, coeffs, times):
+    """M^+ A p for one trajectory (polynomial_optimization_nonlinear_impl.h:162-180): A = blockdiag
+    of setupMappingMatrix(T_i) (lin_impl:102-111), M the 0/1 reordering matrix in the reference's
+    row order (segment i: vertex i derivatives 0..h-1, then vertex i+1; lin_impl:186-213) onto the
+    unique (vertex, derivative) unknowns, M^+ = (M^T M)^-1 M^T.  coeffs [K][D][N] -> [V][h][D]."""
+    coeffs = np.asarray(coeffs, dtype=np.float64)
+    K, D, _ = coeffs.shape
+    h, V = N // 2, K + 1
+    M = np.zeros((K * N, V * h))
+    for i in range(K):
+        for s in range(N):
+            M[i * N + s, (i + (s >= h)) * h + s % h] = 1.0
+    Mp = np.linalg.pinv(M)
+    out = np.zeros((V, h, D))
+    for d in range(D):
+        Ap = np.concatenate([setup_mapping_matrix(N, times[i]) @ coeffs[i, d] for i in range(K)])
+        out[:, :, d] = (Mp @ Ap).reshape(V, h)
+    return out
+
+
+def coefficients_from_vertices(N, x, times):
+    """updateSegmentsFromCompactConstraints (lin_impl:253-273) with every vertex derivative given:
+    c_i = A(T_i)^-1 [x_i; x_{i+1}] with the reference's Schur inverse (lin_impl:133-169).
+    x [V][h][D] -> coeffs [K][D][N]."""
+    x = np.asarray(x, dtype=np.float64)
+    V, h, D = x.shape
+    K = V - 1
+    out = np.zeros((K, D, N))
+    for i in range(K):
+        Ai = invert_mapping_matrix(setup_mapping_matrix(N, times[i]))
+        for d in range(D):
+            out[i, d] = Ai @ np.concatenate([x[i, :, d], x[i + 1, :, d]])
+    return out

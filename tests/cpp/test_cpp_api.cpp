@@ -213,7 +213,59 @@ static void test_errors() {
   EXPECT(threw, "negative time must fail");
 }
 
+// setFreeConstraints round trip and computeInitialSolutionWithoutPositionConstraints (nl_impl:116-187)
+static void test_free_constraints_and_reparametrisation() {
+  const int K = 6, D = 3, N = 10;
+  Vertex::Vector vertices;
+  for (int v = 0; v <= K; ++v) {
+    Vertex vx(D);
+    if (v == 0 || v == K)
+      vx.makeStartOrEnd(std::vector<double>{1.0 * v, 2.0 - v, 0.5}, derivative_order::SNAP);
+    else
+      vx.addConstraint(derivative_order::POSITION, std::vector<double>{1.0 * v + 0.2 * (v % 2), -0.7 * v, 0.3 * v * v});
+    vertices.push_back(vx);
+  }
+  std::vector<double> times{1.1, 0.8, 1.7, 2.2, 0.9, 1.3};
+  PolynomialOptimization<N> opt(D);
+  opt.setupFromVertices(vertices, times, derivative_order::SNAP);
+  opt.solveLinear();
+  Segment::Vector s0;
+  opt.getSegments(&s0);
+  const double cost0 = opt.computeCost();
+  std::vector<std::vector<double>> fc, fx;
+  opt.getFreeConstraints(&fc);
+  opt.getFixedConstraints(&fx);
+  EXPECT(fx.size() == (size_t)D && fx[0].size() == opt.getNumberFixedConstraints(), "fixed shape");
+  opt.setFreeConstraints(fc);  // same values: same polynomials and cost
+  Segment::Vector s1;
+  opt.getSegments(&s1);
+  for (int i = 0; i < K; ++i)
+    for (int d = 0; d < D; ++d)
+      for (int j = 0; j < N; ++j) {
+        const double a = s0[i][d].getCoefficients()[j], b = s1[i][d].getCoefficients()[j];
+        EXPECT(std::fabs(a - b) <= 1e-12 * std::fmax(1.0, std::fabs(a)), "setFreeConstraints coefficient");
+      }
+  EXPECT(std::fabs(opt.computeCost() - cost0) <= 1e-9 * cost0, "cost after setFreeConstraints");
+  const size_t nf0 = opt.getNumberFreeConstraints();
+  computeInitialSolutionWithoutPositionConstraints(&opt);
+  EXPECT(opt.getNumberFreeConstraints() == nf0 + (K - 1), "n_free after releasing positions %zu",
+         opt.getNumberFreeConstraints());
+  Segment::Vector s2;
+  opt.getSegments(&s2);
+  for (int i = 0; i < K; ++i)
+    for (int d = 0; d < D; ++d) {
+      double sc = 0.0, err = 0.0, tp = 1.0;
+      for (int j = 0; j < N; ++j, tp *= times[i]) {
+        sc = std::fmax(sc, std::fabs(s0[i][d].getCoefficients()[j]) * tp);
+        err = std::fmax(err, std::fabs(s0[i][d].getCoefficients()[j] - s2[i][d].getCoefficients()[j]) * tp);
+      }
+      EXPECT(err <= 1e-9 * sc, "re-parametrised trajectory differs: seg %d dim %d (%g)", i, d, err / sc);
+    }
+  EXPECT(std::fabs(opt.computeCost() - cost0) <= 1e-8 * cost0, "cost after re-parametrisation");
+}
+
 int main() {
+  test_free_constraints_and_reparametrisation();
   test_two_vertices_setup();
   test_random_paths<10>(3, 10, 4, 4, 20);
   test_random_paths<8>(2, 6, 3, 2, 10);

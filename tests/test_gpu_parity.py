@@ -348,3 +348,49 @@ def test_time_jacobian_reference_difference(gpu_ctx):
     _, Gr = O.cost_time_jacobian_batch(N, r, xf, times, np.ones((1, K)), dt)
     assert G[0, 0, 4] == 0.0 and G[1, 0, 2] == 0.0 and Gr[0, 0, 4] == 0.0 and Gr[1, 0, 2] == 0.0
     assert np.count_nonzero(G == 0.0) == 2 and np.isfinite(J).all()
+
+
+def test_vertex_maps_vs_oracle(gpu_ctx):
+    """mtg_coefficients_from_vertices_batch (setFreeConstraints + updateSegmentsFromCompactConstraints,
+    lin_impl:253-273) and mtg_vertex_derivatives_batch (M^+ A p, nl_impl:162-180) against the oracle's
+    restatements; feeding the solve's own vertex derivatives back reproduces its coefficients."""
+    from mav_trajectory_generation_cmake_amd import full_vertex_values, random_vertices_batch
+    O = _oracle()
+    for N, r, K, B, gen in ((10, 4, 10, 37, "path"), (12, 3, 20, 9, "rand"), (6, 2, 5, 5, "rand")):
+        if gen == "path":
+            vals, mask, times = _bench_batch(B, seed0=500, K=K, N=N)
+        else:
+            vals, mask, times = random_vertices_batch(N, 3, K, B, [-10, -20, -10], [10, 20, 10], seed0=500)
+        sol = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, free=True)
+        xf = full_vertex_values(vals, mask, sol["free"], N)
+        c = gpu_ctx.coefficients_from_vertices_batch(N, xf, times)
+        assert scale_normalised_error(c, sol["coeffs"], times) <= 1e-12, N
+        x2 = gpu_ctx.vertex_derivatives_batch(sol["coeffs"], times)
+        scale = np.max(np.abs(xf), axis=(1, 2), keepdims=True)  # per trajectory and dimension
+        assert np.max(np.abs(x2 - xf) / scale) <= 1e-9, N
+        for b in (0, B - 1):
+            cr = O.coefficients_from_vertices(N, xf[b], times[b])
+            assert scale_normalised_error(c[b:b + 1], cr[None], times[b:b + 1]) <= 1e-8, (N, b)
+            xr = O.vertex_derivatives(N, sol["coeffs"][b], times[b])
+            assert np.max(np.abs(x2[b] - xr) / scale[b]) <= 1e-9, (N, b)
+
+
+def test_initial_solution_without_position_constraints(gpu_ctx):
+    """computeInitialSolutionWithoutPositionConstraints (nl_impl:116-187): interior positions become
+    free, the new free vector comes from the solved trajectory, and setting it back
+    (setFreeConstraints) reproduces the same polynomials; the free vector matches the oracle's
+    M^+ A p in the reference order."""
+    O = _oracle()
+    N, r, K, B = 10, 4, 10, 16
+    vals, mask, times = _bench_batch(B, seed0=900, K=K)
+    out = gpu_ctx.initial_solution_without_position_constraints(N, r, vals, mask, times)
+    assert np.all(out["mask"][:, 1:K] & 1 == 0) and np.all(out["mask"][:, [0, K]] == mask[:, [0, K]])
+    assert np.all(out["n_free"] == 9 * 5)  # 9 interior vertices x 5 derivatives
+    c = gpu_ctx.set_free_constraints_batch(N, out["values"], out["mask"], times, out["free"])
+    assert scale_normalised_error(c, out["coeffs"], times) <= 1e-9
+    for b in (0, 7):
+        xr = O.vertex_derivatives(N, out["coeffs"][b], times[b])
+        fixed = ((out["mask"][b][:, None] >> np.arange(5)) & 1).astype(bool)
+        fr = xr.reshape(-1, 3)[np.flatnonzero(~fixed.reshape(-1))].T  # [D][n_free]
+        sc = np.max(np.abs(fr), axis=1, keepdims=True)
+        assert np.max(np.abs(out["free"][b][:, :45] - fr) / sc) <= 1e-9, b

@@ -309,3 +309,16 @@ def _time_jacobian_checks(mp):
         want = 0.0 if times2[0, n] <= 0.1 else (Jpm[0, 0] - Jpm[0, 1]) / (2 * dt)
         assert abs(G2[0, 0, n] - want) <= 1e-9 * max(abs(J2[0, 0]), 1.0) / dt, (n, G2[0, 0, n], want)
     assert G2[0, 0, 1] == 0.0
+
+
+def test_vertex_maps_oracle_round_trip():
+    """coefficients_from_vertices (lin_impl:253-273) then M^+ A p (nl_impl:162-180) returns the vertex
+    derivatives: A_i c_i reproduces both segment ends, so the pseudo-inverse's average is exact."""
+    rng = np.random.default_rng(11)
+    for N, K, D in ((10, 4, 3), (6, 3, 2), (12, 2, 1)):
+        h = N // 2
+        x = rng.uniform(-2, 2, size=(K + 1, h, D))
+        times = rng.uniform(0.5, 3.0, size=K)
+        c = O.coefficients_from_vertices(N, x, times)
+        back = O.vertex_derivatives(N, c, times)
+        np.testing.assert_allclose(back, x, rtol=1e-8, atol=1e-9 * np.abs(x).max())
