@@ -70,15 +70,16 @@ def max_over_ranks(x, dist, device):
     return float(t.item())
 
 
-def traffic_from_profiles(kernel_prefix, batch):
-    """HBM bytes per launch of the solve kernel from the committed PMC summary (profiles/), or None."""
+def traffic_from_profiles(kernel_prefix, batch, workload):
+    """HBM bytes per launch of the kernel from the committed PMC summary (profiles/), or None.  Keyed
+    by kernel and workload (scripts/summarize_profiles.py)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        ent = d.get(kernel_prefix, {}).get(str(batch))
+        ent = d.get("%s|%s" % (kernel_prefix, workload), {}).get(str(batch))
         return None if ent is None else float(ent["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -252,7 +253,7 @@ def main():
     total = units * world * args.steps
     value = total / el
     achieved = bpt * B / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profiles(kname, B)
+    traffic = traffic_from_profiles(kname, B, wl)
     out = {
         "metric": metric,
         "value": value,

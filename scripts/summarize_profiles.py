@@ -12,7 +12,9 @@ gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md "HBM [CDNA4]" (FETCH_SIZE = 
 with 128-B requests).  Infinity-Cache (L3) hits are counted by these counters, so at sizes whose
 inputs stay L3-resident between launches this over-states true HBM bytes.
 
-usage: summarize_profiles.py TAG B [B ...]      (reads gpurun_out/prof<SRC>_b<B>, SRC from $PROF_SRC)
+usage: summarize_profiles.py TAG B [B ...]      (reads gpurun_out/prof<SRC>_b<B>, SRC from $PROF_SRC;
+       $WORKLOAD names the bench workload profiled, default config2: traffic is keyed
+       "<kernel>|<workload>" so a kernel profiled on one workload is not quoted for another)
 """
 import csv
 import json
@@ -75,7 +77,8 @@ def main():
                 ent["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0)
             summary["kernels"][k] = ent
             if "hbm_bytes_per_launch" in ent:
-                traffic.setdefault(short(k), {})[str(B)] = {
+                key = "%s|%s" % (short(k), os.environ.get("WORKLOAD", "config2"))
+                traffic.setdefault(key, {})[str(B)] = {
                     "hbm_bytes_per_launch": ent["hbm_bytes_per_launch"],
                     "fetch_kib_raw": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
                     "l2_hit_rate": ent.get("l2_hit_rate"), "profile": "%s_b%s_pmc.json" % (tag, B)}
