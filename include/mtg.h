@@ -183,6 +183,26 @@ int mtg_coefficients_from_vertices_batch(mtg_ctx* ctx, int N, int D, int K, int6
 int mtg_vertex_derivatives_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
                                  const double* times, double* vertex_values, unsigned flags);
 
+/* Extremum of a trajectory (the reference's Extremum, extremum.h): segment-local time, value and
+ * segment index. */
+typedef struct mtg_extremum {
+  double time;
+  double value;
+  int32_t segment;
+  int32_t reserved;
+} mtg_extremum;
+
+/* Minimum and maximum magnitude of derivative `derivative` (0 <= derivative <= N-2) over each
+ * whole trajectory: Trajectory::computeMinMaxMagnitude (src/trajectory.cpp:181-218) with the
+ * dimensions in dimension_mask (bit d = dimension d; 0 = all).  Per segment the candidates are
+ * t = 0, t = T and the real roots in [0, T] of sum_d conv(p_d^(k), p_d^(k+1)) (one dimension: of
+ * p^(k+1)), src/segment.cpp:82-196.  coeffs [B][K][D][N], times [B][K]; minimum / maximum [B]
+ * (either may be NULL).  Roots are isolated on 256 samples per segment and refined to a few ulp
+ * (the reference uses Jenkins-Traub, src/rpoly.cpp); see DESIGN.md. */
+int mtg_min_max_magnitude_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                const double* times, int derivative, uint32_t dimension_mask,
+                                mtg_extremum* minimum, mtg_extremum* maximum, unsigned flags);
+
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);

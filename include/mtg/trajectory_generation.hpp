@@ -221,6 +221,39 @@ class Trajectory {
     if (sampling_times) sampling_times->assign(st.begin(), st.begin() + count);
   }
 
+  // Trajectory::computeMinMaxMagnitude (src/trajectory.cpp:181-218), on the GPU
+  // (mtg_min_max_magnitude_batch); Extremum as in the reference (extremum.h): segment-local time,
+  // value, segment index
+  struct Extremum {
+    double time = 0.0, value = 0.0;
+    int segment_idx = -1;
+  };
+  bool computeMinMaxMagnitude(int derivative, const std::vector<int>& dimensions, Extremum* minimum,
+                              Extremum* maximum) const {
+    if (segments_.empty() || dimensions.empty()) return false;
+    const int K = this->K(), D = this->D(), N = this->N();
+    std::vector<double> coeffs((size_t)K * D * N), times(K);
+    for (int i = 0; i < K; ++i) {
+      times[i] = segments_[i].getTime();
+      for (int d = 0; d < D; ++d) {
+        const auto& c = segments_[i][d].getCoefficients();
+        std::copy(c.begin(), c.end(), coeffs.begin() + ((size_t)i * D + d) * N);
+      }
+    }
+    uint32_t mask = 0;
+    for (int d : dimensions) {
+      if (d < 0 || d >= D) return false;  // segment.cpp:101-106: out-of-range dimension
+      mask |= 1u << d;
+    }
+    mtg_ctx* ctx = default_context();
+    mtg_extremum mn, mx;
+    check(mtg_min_max_magnitude_batch(ctx, N, D, K, 1, coeffs.data(), times.data(), derivative, mask, &mn, &mx, 0),
+          ctx, "mtg_min_max_magnitude_batch");
+    *minimum = Extremum{mn.time, mn.value, mn.segment};
+    *maximum = Extremum{mx.time, mx.value, mx.segment};
+    return true;
+  }
+
  private:
   Segment::Vector segments_;
 };
@@ -482,6 +515,12 @@ class BatchPolynomialOptimization {
                          unsigned flags = 0) {
     check(mtg_vertex_derivatives_batch(ctx_, N, D_, K_, batch, coeffs, times, vertex_values, flags), ctx_,
           "mtg_vertex_derivatives_batch");
+  }
+  void minMaxMagnitude(int64_t batch, const double* coeffs, const double* times, int derivative,
+                       uint32_t dimension_mask, mtg_extremum* minimum, mtg_extremum* maximum, unsigned flags = 0) {
+    check(mtg_min_max_magnitude_batch(ctx_, N, D_, K_, batch, coeffs, times, derivative, dimension_mask, minimum,
+                                      maximum, flags),
+          ctx_, "mtg_min_max_magnitude_batch");
   }
   mtg_ctx* context() const { return ctx_; }
 

@@ -65,6 +65,9 @@ _SIGNATURES = {
                                                             ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
     "mtg_vertex_derivatives_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                     ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_min_max_magnitude_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int, ctypes.c_uint32,
+                                                   _c_dp, _c_dp, ctypes.c_uint]),
     "mtg_last_kernel_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "mtg_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mtg_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,

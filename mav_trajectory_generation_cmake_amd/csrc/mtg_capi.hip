@@ -510,6 +510,58 @@ int mtg_vertex_derivatives_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batc
   return run_vertex_map(ctx, false, N, D, K, batch, coeffs, times, vertex_values, flags);
 }
 
+int mtg_min_max_magnitude_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                const double* times, int derivative, uint32_t dimension_mask,
+                                mtg_extremum* minimum, mtg_extremum* maximum, unsigned flags) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  if (N < 2 || N > 12 || (N % 2)) return set_error(ctx, MTG_ERR_UNSUPPORTED_N, "N must be even and in [2, 12]");
+  if (K < 1 || D < 1 || batch < 0) return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "need K >= 1, D >= 1, batch >= 0");
+  if (K > 256) return set_error(ctx, MTG_ERR_TOO_LARGE, "K must be <= 256");
+  if (derivative < 0 || derivative > N - 2)
+    return set_error(ctx, MTG_ERR_BAD_DERIVATIVE, "derivative must be in [0, N-2] (polynomial.cpp:62-65)");
+  const uint32_t all = D >= 32 ? 0xffffffffu : ((1u << D) - 1u);
+  const uint32_t dims = dimension_mask ? dimension_mask : all;
+  if (D > 32 || (dims & ~all)) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "dimension_mask out of range");
+  if (batch == 0) return MTG_OK;
+  if (!coeffs || !times) return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "coeffs and times are required");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const size_t b_coef = sizeof(double) * (size_t)batch * K * D * N, b_times = sizeof(double) * (size_t)batch * K,
+               b_ext = sizeof(mtg_extremum) * (size_t)batch;
+  const double *d_coef = coeffs, *d_times = times;
+  mtg_extremum *d_min = minimum, *d_max = maximum;
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  char* base = nullptr;
+  size_t o_min = 0, o_max = 0;
+  if (!dev) {
+    size_t off = 0;
+    const size_t o_coef = off; off = align_up(off + b_coef);
+    const size_t o_times = off; off = align_up(off + b_times);
+    o_min = off; off = align_up(off + b_ext);
+    o_max = off; off = align_up(off + b_ext);
+    MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
+    base = static_cast<char*>(ctx->staging);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coef, coeffs, b_coef, hipMemcpyHostToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+    d_coef = reinterpret_cast<const double*>(base + o_coef);
+    d_times = reinterpret_cast<const double*>(base + o_times);
+    d_min = minimum ? reinterpret_cast<mtg_extremum*>(base + o_min) : nullptr;
+    d_max = maximum ? reinterpret_cast<mtg_extremum*>(base + o_max) : nullptr;
+  }
+  MTG_HIP_TRY(ctx, time_begin(ctx));
+  MTG_HIP_TRY(ctx, mtg::launch_min_max_magnitude(N, d_coef, d_times, batch, K, D, derivative, dims, d_min, d_max,
+                                                 ctx->stream));
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  if (!dev) {
+    if (minimum) MTG_HIP_TRY(ctx, hipMemcpyAsync(minimum, base + o_min, b_ext, hipMemcpyDeviceToHost, ctx->stream));
+    if (maximum) MTG_HIP_TRY(ctx, hipMemcpyAsync(maximum, base + o_max, b_ext, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  } else if (!(flags & MTG_FLAG_ASYNC)) {
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return MTG_OK;
+}
+
 int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
                              const double* coeffs, const double* times, double t_start,
                              double t_end, double dt, int derivative, int64_t* counts,

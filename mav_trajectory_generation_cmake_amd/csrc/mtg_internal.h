@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mtg.h"
+
 namespace mtg {
 
 // Arguments of one batched solve launch.  Pointers are device pointers.
@@ -55,6 +57,11 @@ hipError_t launch_time_jacobian(int N, int r, const double* values, const double
 bool vertex_map_fits(int N, int D, int K);
 hipError_t launch_vertex_map(bool to_coeffs, int N, const double* in, const double* times, double* out, int64_t B,
                              int K, int D, hipStream_t stream);
+
+// min / max magnitude of a derivative over trajectories (mtg_extrema.hip)
+hipError_t launch_min_max_magnitude(int N, const double* coeffs, const double* times, int64_t B, int K, int D,
+                                    int derivative, unsigned dims, mtg_extremum* mn, mtg_extremum* mx,
+                                    hipStream_t stream);
 
 // evaluateRange
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,

@@ -27,6 +27,10 @@ def _addr(x):
     return x.ctypes.data
 
 
+# struct mtg_extremum (include/mtg.h)
+EXTREMUM_DTYPE = np.dtype([("time", "<f8"), ("value", "<f8"), ("segment", "<i4"), ("reserved", "<i4")])
+
+
 class Context:
     """Owns one mtg_ctx (a HIP stream + staging buffers on one device)."""
 
@@ -310,6 +314,22 @@ class Context:
             n_free[b] = len(slots)
             free[b, :, :len(slots)] = allv[b].reshape(-1, D)[slots].T
         return {"mask": new_mask, "values": values, "free": free, "n_free": n_free, "coeffs": sol["coeffs"]}
+
+    def min_max_magnitude_batch(self, coeffs, times, derivative, dimensions=None):
+        """Trajectory::computeMinMaxMagnitude (src/trajectory.cpp:181-218) for a batch (include/mtg.h
+        mtg_min_max_magnitude_batch).  Returns (minimum, maximum), structured arrays [B] with fields
+        time (segment-local), value, segment."""
+        coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+        times = np.ascontiguousarray(times, dtype=np.float64)
+        B, K, D, N = coeffs.shape
+        mask = 0 if dimensions is None else int(sum(1 << int(d) for d in dimensions))
+        mn = np.zeros(B, dtype=EXTREMUM_DTYPE)
+        mx = np.zeros(B, dtype=EXTREMUM_DTYPE)
+        self.reset_stream()
+        nat.check(self._lib.mtg_min_max_magnitude_batch(self.handle, N, D, K, B, _addr(coeffs), _addr(times),
+                                                        int(derivative), mask, _addr(mn), _addr(mx), 0),
+                  self.handle)
+        return mn, mx
 
     # ------------------------------------------------------- evaluateRange
     def evaluate_range_batch(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True):

@@ -298,3 +298,66 @@ def coefficients_from_vertices(N, x, times):
         for d in range(D):
             out[i, d] = Ai @ np.concatenate([x[i, :, d], x[i + 1, :, d]])
     return out
+
+
+def _real_roots_in(poly_inc, t0, t1):
+    """Real roots in [t0, t1] of a polynomial with INCREASING coefficients, selected as
+    Polynomial::selectMinMaxCandidatesFromRoots does (src/polynomial.cpp:27-55: |imag| <= eps).
+    The reference's root finder is Jenkins-Traub (src/rpoly.cpp); here LAPACK's companion-matrix
+    eigenvalues (numpy.roots), which likewise return exactly-zero imaginary parts for roots it
+    computes as real."""
+    c = np.trim_zeros(np.asarray(poly_inc, dtype=np.float64), "b")
+    if len(c) <= 1:
+        return []
+    r = np.roots(c[::-1])
+    out = []
+    for z in r:
+        if abs(z.imag) > np.finfo(float).eps:
+            continue
+        if t0 <= z.real <= t1:
+            out.append(float(z.real))
+    return out
+
+
+def min_max_magnitude(N, coeffs, times, derivative, dims=None):
+    """Trajectory::computeMinMaxMagnitude (src/trajectory.cpp:181-218) for one trajectory.
+    coeffs [K][D][N] -> ((t, value, segment) minimum, (t, value, segment) maximum)."""
+    from math import factorial
+    coeffs = np.asarray(coeffs, dtype=np.float64)
+    K, D, _ = coeffs.shape
+    dims = list(range(D)) if dims is None else list(dims)
+    k = derivative
+
+    def dcoef(c, m):  # getCoefficients(m): derivative coefficients, increasing powers
+        return np.array([c[j + m] * factorial(j + m) / factorial(j) for j in range(N - m)])
+
+    def mag(i, t):
+        s = 0.0
+        for d in dims:
+            s += np.polyval(dcoef(coeffs[i, d], k)[::-1], t) ** 2
+        return np.sqrt(s)
+
+    mn, mx = (0.0, np.finfo(float).max, 0), (0.0, -np.finfo(float).max, 0)
+    for i in range(K):
+        T = float(times[i])
+        if len(dims) > 1:  # segment.cpp:96-122
+            nd, ndd = N - k, N - k - 1
+            conv = np.zeros(nd + ndd - 1)
+            for d in dims:
+                conv += np.convolve(dcoef(coeffs[i, d], k)[:nd], dcoef(coeffs[i, d], k + 1)[:ndd])
+            roots = _real_roots_in(conv, 0.0, T)
+        else:  # one dimension: roots of p^(k+1) (segment.cpp:124-130)
+            roots = _real_roots_in(dcoef(coeffs[i, dims[0]], k + 1), 0.0, T)
+        cands = [0.0, T] + roots + [0.0, T]  # candidates, then start / end again (segment.cpp:172-193)
+        smin, smax = (0.0, np.finfo(float).max), (0.0, -np.finfo(float).max)
+        for t in cands:
+            v = mag(i, t)
+            if smax[1] < v:
+                smax = (t, v)
+            if v < smin[1]:
+                smin = (t, v)
+        if smin[1] < mn[1]:
+            mn = (smin[0], smin[1], i)
+        if smax[1] > mx[1]:
+            mx = (smax[0], smax[1], i)
+    return mn, mx

@@ -177,6 +177,17 @@ static void test_evaluate_range() {
   std::vector<double> st;
   traj.evaluateRange(0.0, traj.getMaxTime(), 0.01, derivative_order::POSITION, &samples, &st);
   EXPECT(samples.size() == st.size() && samples.size() >= 449 && samples.size() <= 451, "samples %zu", samples.size());
+  // computeMinMaxMagnitude (trajectory.cpp:181-218) against the sampled speed
+  Trajectory::Extremum vmin, vmax;
+  EXPECT(traj.computeMinMaxMagnitude(derivative_order::VELOCITY, {0, 1}, &vmin, &vmax), "min/max magnitude");
+  std::vector<std::vector<double>> vel;
+  traj.evaluateRange(0.0, traj.getMaxTime(), 0.001, derivative_order::VELOCITY, &vel);
+  double smax = 0.0;
+  for (const auto& v : vel) smax = std::fmax(smax, std::sqrt(v[0] * v[0] + v[1] * v[1]));
+  EXPECT(vmax.value >= smax * (1 - 1e-12) && vmax.value <= smax * (1 + 1e-4), "max speed %g vs sampled %g", vmax.value,
+         smax);
+  EXPECT(vmin.value <= 1e-9 && vmax.segment_idx >= 0 && vmax.segment_idx < 3, "min speed %g (rest at the ends)",
+         vmin.value);
   for (size_t s = 0; s < samples.size(); s += 37) {
     const auto e = traj.evaluate(st[s], derivative_order::POSITION);
     for (int d = 0; d < 2; ++d)

@@ -15,8 +15,9 @@ pytestmark = pytest.mark.skipif(not os.path.exists(hipcc), reason="hipcc not ava
 
 def _device_asm(src, tmp_path):
     out = tmp_path / (os.path.basename(src) + ".s")
-    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                    os.path.join(CSRC, src), "-o", str(out)], check=True, capture_output=True)
+    inc = os.path.join(os.path.dirname(os.path.dirname(CSRC)), "include")
+    subprocess.run([hipcc, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-I", inc,
+                    "-I", CSRC, os.path.join(CSRC, src), "-o", str(out)], check=True, capture_output=True)
     return out.read_text()
 
 

@@ -394,3 +394,22 @@ def test_initial_solution_without_position_constraints(gpu_ctx):
         fr = xr.reshape(-1, 3)[np.flatnonzero(~fixed.reshape(-1))].T  # [D][n_free]
         sc = np.max(np.abs(fr), axis=1, keepdims=True)
         assert np.max(np.abs(out["free"][b][:, :45] - fr) / sc) <= 1e-9, b
+
+
+@pytest.mark.parametrize("derivative,dims", [(1, None), (2, None), (1, [1]), (3, [0, 2])])
+def test_min_max_magnitude_vs_oracle(gpu_ctx, derivative, dims):
+    """mtg_min_max_magnitude_batch against the oracle's Trajectory::computeMinMaxMagnitude
+    (src/trajectory.cpp:181-218; real roots of the convolved derivative polynomial)."""
+    O = _oracle()
+    N, r, K, B = 10, 4, 10, 48
+    vals, mask, times = _bench_batch(B, seed0=1200, K=K)
+    coeffs = gpu_ctx.solve_linear_batch(N, r, vals, mask, times)["coeffs"]
+    mn, mx = gpu_ctx.min_max_magnitude_batch(coeffs, times, derivative, dims)
+    for b in range(B):
+        rmn, rmx = O.min_max_magnitude(N, coeffs[b], times[b], derivative, dims)
+        for got, ref in ((mx[b], rmx), (mn[b], rmn)):
+            scale = max(abs(rmx[1]), 1e-300)
+            assert abs(got["value"] - ref[1]) <= 1e-9 * scale, (b, got, ref)
+            if got["segment"] == ref[2]:
+                # the extremum's time: a root refined to a few ulp (flat extrema: value-equivalent)
+                assert abs(got["time"] - ref[0]) <= 1e-6 * times[b, ref[2]] or abs(got["value"] - ref[1]) <= 1e-12 * scale

@@ -322,3 +322,22 @@ def test_vertex_maps_oracle_round_trip():
         c = O.coefficients_from_vertices(N, x, times)
         back = O.vertex_derivatives(N, c, times)
         np.testing.assert_allclose(back, x, rtol=1e-8, atol=1e-9 * np.abs(x).max())
+
+
+def test_min_max_magnitude_oracle_vs_sampling():
+    """computeMinMaxMagnitude's candidates against dense sampling, as the reference's own test checks
+    its root-based extrema (test/test_polynomial_optimization.cpp:447-487, sampling at 1e-3 s)."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, 6, 3, seed0=70)
+    for b in range(3):
+        r = O.solve_linear(10, 4, vals[b], mask[b].astype(np.uint32), times[b])
+        c = r["coeffs"]
+        for k in (1, 2):
+            mn, mx = O.min_max_magnitude(10, c, times[b], k)
+            best_hi, best_lo = -1.0, np.inf
+            for i in range(6):
+                t = np.linspace(0.0, times[b, i], 4001)
+                m = np.sqrt(sum(np.polyval(np.polyder(c[i, d][::-1], k), t) ** 2 for d in range(3)))
+                best_hi, best_lo = max(best_hi, m.max()), min(best_lo, m.min())
+            assert best_hi <= mx[1] * (1 + 1e-12) and mx[1] <= best_hi * (1 + 1e-5), (b, k, mx, best_hi)
+            assert mn[1] <= best_lo * (1 + 1e-12) + 1e-12 and best_lo <= mn[1] + 1e-5 * best_hi, (b, k, mn, best_lo)
