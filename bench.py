@@ -135,8 +135,10 @@ def make_problems(workload, N, K, B, seed0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults: enough warmup for the GPU clocks to settle (a 10-launch warmup left the B = 131072
+    # kernel at 195 us instead of 155 us), and a timed region of ~15 ms at config 2
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2")
     ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (configs 2, 4, 5: 1e4)")
     ap.add_argument("--segments", type=int, default=None)

@@ -29,6 +29,13 @@ struct mtg_ctx {
   std::mutex mu;
 };
 
+namespace mtg {
+PendingEvents& pending_events() {
+  static thread_local PendingEvents pe;
+  return pe;
+}
+}  // namespace mtg
+
 namespace {
 
 int set_hip_error(mtg_ctx* ctx, hipError_t e, const char* what) {
@@ -66,14 +73,34 @@ hipError_t ensure(void** buf, size_t* have, size_t need) {
   return e;
 }
 
-hipError_t time_begin(mtg_ctx* ctx) {
+// Timed region around one launch.  single: the call launches exactly one kernel through
+// mtg::launch_kernel, which carries the event pair in its dispatch packet; otherwise (the split
+// path's two kernels) the events are recorded as stream markers around the launches.
+hipError_t time_begin(mtg_ctx* ctx, bool single = true) {
   const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
+  mtg::PendingEvents& pe = mtg::pending_events();
+  pe = mtg::PendingEvents{};
+  if (single) {
+    pe.start = ctx->ev_start[slot];
+    pe.stop = ctx->ev_stop[slot];
+    return hipSuccess;
+  }
   return hipEventRecord(ctx->ev_start[slot], ctx->stream);
 }
 
 hipError_t time_end(mtg_ctx* ctx) {
   const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
-  hipError_t e = hipEventRecord(ctx->ev_stop[slot], ctx->stream);
+  mtg::PendingEvents& pe = mtg::pending_events();
+  hipError_t e = hipSuccess;
+  if (pe.start) {
+    if (!pe.used) {  // nothing was launched (e.g. an empty batch): an empty interval
+      e = hipEventRecord(pe.start, ctx->stream);
+      if (e == hipSuccess) e = hipEventRecord(pe.stop, ctx->stream);
+    }
+    pe = mtg::PendingEvents{};
+  } else {
+    e = hipEventRecord(ctx->ev_stop[slot], ctx->stream);
+  }
   if (e == hipSuccess) ctx->launches++;
   return e;
 }
@@ -184,7 +211,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     // entries beyond n_free are left zero
     MTG_HIP_TRY(ctx, hipMemsetAsync(const_cast<double*>(a.free_out), 0, b_free, ctx->stream));
   }
-  MTG_HIP_TRY(ctx, time_begin(ctx));
+  MTG_HIP_TRY(ctx, time_begin(ctx, !(flags & MTG_FLAG_SPLIT_KERNELS)));
   if (flags & MTG_FLAG_SPLIT_KERNELS) {
     const size_t ws = mtg::split_workspace_bytes(N, D, K, pairs);
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));

@@ -153,7 +153,7 @@ hipError_t launch_cost_nr(const CostArgs& a, hipStream_t stream) {
   const size_t lds = sizeof(double) * ((size_t)a.K * a.D * (2 * H - 1) + a.K + (size_t)(a.K + 1) * H * a.D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   if (a.B == 0) return hipSuccess;
-  hipLaunchKernelGGL((cost_at_times_kernel<N, R>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
+  launch_kernel((cost_at_times_kernel<N, R>), dim3((unsigned)a.B), dim3(64), lds, stream, a);
   return hipGetLastError();
 }
 

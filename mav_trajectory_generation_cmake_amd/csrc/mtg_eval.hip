@@ -332,7 +332,7 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
   const int block = 256;
   const int64_t grid = (B + block - 1) / block;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL(eval_count_kernel, dim3((unsigned)grid), dim3(block), 0, stream, K, B, times, t_start,
+  launch_kernel(eval_count_kernel, dim3((unsigned)grid), dim3(block), 0, stream, K, B, times, t_start,
                      t_end, dt, counts);
   return hipGetLastError();
 }
@@ -345,7 +345,7 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   if (lds > 64 * 1024) return hipErrorInvalidValue;
 #define MTG_EVAL_CASE(NN)                                                                               \
   case NN:                                                                                              \
-    hipLaunchKernelGGL(eval_range_kernel<NN>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, \
+    launch_kernel(eval_range_kernel<NN>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, \
                        coeffs, times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times);     \
     break;
   switch (N) {

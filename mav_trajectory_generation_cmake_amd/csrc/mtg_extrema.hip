@@ -162,7 +162,7 @@ hipError_t launch_extrema_n(const double* coeffs, const double* times, int64_t B
                             mtg_extremum* mn, mtg_extremum* mx, hipStream_t stream) {
   const int tpb = kExtremaThreads / K;
   const dim3 grid((unsigned)((B + tpb - 1) / tpb)), block(kExtremaThreads);
-  hipLaunchKernelGGL((min_max_magnitude_kernel<N>), grid, block, 0, stream, coeffs, times, B, K, D, k, dims, mn, mx);
+  launch_kernel((min_max_magnitude_kernel<N>), grid, block, 0, stream, coeffs, times, B, K, D, k, dims, mn, mx);
   return hipGetLastError();
 }
 

@@ -2,12 +2,34 @@
 // (mtg_capi.hip).  Not installed; the public surface is include/mtg.h.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "mtg.h"
 
 namespace mtg {
+
+// Timing events for the next kernel launch, set by the C ABI around a timed call: launch_kernel()
+// records them in the kernel's own dispatch packet (hipExtLaunchKernelGGL) instead of as two
+// separate marker packets in the stream.
+struct PendingEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool used = false;
+};
+PendingEvents& pending_events();  // per host thread
+
+template <typename F, typename... Args>
+inline void launch_kernel(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t stream,
+                          Args... args) {
+  PendingEvents& pe = pending_events();
+  if (pe.start && !pe.used) {
+    pe.used = true;
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, pe.start, pe.stop, 0u, args...);
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+  }
+}
 
 // Arguments of one batched solve launch.  Pointers are device pointers.
 struct SolveArgs {

@@ -389,7 +389,7 @@ static hipError_t launch_fused_nr(const SolveArgs& a, hipStream_t stream) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((solve_fused_kernel<N, R>), dim3((unsigned)blocks), dim3(kBlock), lds, stream, a, lg_log2);
+  launch_kernel((solve_fused_kernel<N, R>), dim3((unsigned)blocks), dim3(kBlock), lds, stream, a, lg_log2);
   return hipGetLastError();
 }
 

@@ -169,9 +169,9 @@ hipError_t launch_vertex_n(bool to_coeffs, const double* in, const double* times
   const size_t lds = sizeof(double) * (size_t)tb * ((size_t)V * H * D + K + (size_t)K * D * N);
   const dim3 grid((unsigned)((B + tb - 1) / tb)), block(kVtxThreads);
   if (to_coeffs)
-    hipLaunchKernelGGL((coefficients_from_vertices_kernel<N>), grid, block, lds, stream, in, times, out, B, K, D, tb);
+    launch_kernel((coefficients_from_vertices_kernel<N>), grid, block, lds, stream, in, times, out, B, K, D, tb);
   else
-    hipLaunchKernelGGL((vertex_derivatives_kernel<N>), grid, block, lds, stream, in, times, out, B, K, D, tb);
+    launch_kernel((vertex_derivatives_kernel<N>), grid, block, lds, stream, in, times, out, B, K, D, tb);
   return hipGetLastError();
 }
 
