@@ -280,6 +280,19 @@ def main():
                      "algorithmic_bytes_per_traj": bpt},
         "cpu_baseline": None,
     }
+    # end-to-end (not `value`): host arrays in and out through the C ABI's staging -- H2D, kernel,
+    # D2H, synchronize -- the PCIe-inclusive rate of a caller that holds its batch in host memory
+    if wl != "config5":
+        for _ in range(3):
+            ctx.solve_linear_batch(N, r, values, mask, times)
+        e2e_n = 20
+        t0 = time.perf_counter()
+        for _ in range(e2e_n):
+            ctx.solve_linear_batch(N, r, values, mask, times)
+        e2e_s = (time.perf_counter() - t0) / e2e_n
+        out["end_to_end"] = {"value": B / e2e_s, "unit": unit, "ms_per_step": e2e_s * 1e3,
+                             "note": "per GPU; host arrays in/out (H2D %d B + D2H %d B per trajectory), synchronous"
+                                     % (bpt - K * D * N * 8, K * D * N * 8)}
     if rank == 0 and not args.no_cpu_baseline:
         threads = int(os.environ.get("MTG_CPU_THREADS", min(16, os.cpu_count() or 1)))
         S = min(args.cpu_sample, B)

@@ -413,3 +413,42 @@ def test_min_max_magnitude_vs_oracle(gpu_ctx, derivative, dims):
             if got["segment"] == ref[2]:
                 # the extremum's time: a root refined to a few ulp (flat extrema: value-equivalent)
                 assert abs(got["time"] - ref[0]) <= 1e-6 * times[b, ref[2]] or abs(got["value"] - ref[1]) <= 1e-12 * scale
+
+
+def test_interior_waypoint_path_with_mixed_end_masks(gpu_ctx):
+    """The register kernel's interior-waypoint path (K == KMAX, every interior vertex fixes exactly its
+    position) with end masks that differ inside a wave, and a batch where some waves break the
+    interior pattern: every trajectory still matches the oracle and the general kernel."""
+    O = _oracle()
+    N, r, K, B = 10, 4, 10, 67
+    vals, mask, times = _bench_batch(B, seed0=4242, K=K)
+    mask = mask.copy()
+    rng = np.random.default_rng(17)
+    # ends: position plus a random subset of the other derivatives (differs per trajectory)
+    mask[:, 0] = 1 | (rng.integers(0, 32, size=B).astype(np.uint8) & 0x1E)
+    mask[:, K] = 1 | (rng.integers(0, 32, size=B).astype(np.uint8) & 0x1E)
+    # trajectories 20 and 45 fix a velocity at an interior vertex: their waves take the generic path
+    mask[20, 4] |= 2
+    mask[45, 7] |= 2
+    vals[20, 4, 1] = 0.3
+    vals[45, 7, 1] = -0.2
+    ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
+    out = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, status=True, cost=True, free=True, n_free=True)
+    gen = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, general=True, cost=True, free=True, n_free=True)
+    assert np.all(out["status"] == 0)
+    assert scale_normalised_error(out["coeffs"], ref, times) <= 1e-6
+    assert scale_normalised_error(out["coeffs"], gen["coeffs"], times) <= 1e-9
+    np.testing.assert_array_equal(out["n_free"], gen["n_free"])
+    np.testing.assert_allclose(out["cost"], gen["cost"], rtol=1e-9)
+
+
+def test_sharded_solves_bitwise_equal(gpu_ctx):
+    """results on G shards must be bit-identical to one batch for the same trajectories
+    (contiguous shards as bench.py gives the ranks, split at a non-multiple of the 8-trajectory wave)."""
+    vals, mask, times = _bench_batch(101, seed0=77)
+    whole = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, cost=True)
+    for cut in (37, 64):
+        a = gpu_ctx.solve_linear_batch(10, 4, vals[:cut], mask[:cut], times[:cut], cost=True)
+        b = gpu_ctx.solve_linear_batch(10, 4, vals[cut:], mask[cut:], times[cut:], cost=True)
+        np.testing.assert_array_equal(np.concatenate([a["coeffs"], b["coeffs"]]), whole["coeffs"])
+        np.testing.assert_array_equal(np.concatenate([a["cost"], b["cost"]]), whole["cost"])
