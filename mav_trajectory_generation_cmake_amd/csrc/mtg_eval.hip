@@ -229,7 +229,8 @@ struct RunLds {  // structure of arrays in LDS
 // One wave per trajectory: lane 0 turns the clock into runs (a few tens per segment), all lanes
 // evaluate the runs' samples -- consecutive samples on consecutive lanes -- with the coefficients
 // staged in LDS.
-template <int N>
+// DER >= 0: the derivative order at compile time (0..4, the common ones); DER < 0: `derivative`.
+template <int N, int DER>
 __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, const double* coeffs,
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
@@ -247,10 +248,11 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
   double* cf = reinterpret_cast<double*>(rt + 1);  // [K][D][N]
   double* ob = cf + K * D * N;                     // [kEvalThreads][D] output block
   const double* cb = coeffs + b * (int64_t)K * D * N;
-  for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = cb[i];
-  double row[N];
-#pragma unroll
-  for (int j = 0; j < N; ++j) row[j] = base_coeff(derivative, j);
+  if (DER >= 0) derivative = DER;
+  // the Horner terms base_coefficients_(derivative, j) * coefficients_[j] (polynomial.h:143-148) do
+  // not depend on t: formed once per coefficient here, with the same rounding as the reference's
+  // per-sample products
+  for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = base_coeff(derivative, i % N) * cb[i];
   const int64_t base = offsets[b];
   Clock ck;
   if (lane == 0) ck.init(times + b * K, K, t_start, t_end, dt);
@@ -287,33 +289,33 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
       const int64_t n = nb + lane;
       const int cnt = (int)(end - nb < kEvalThreads ? end - nb : kEvalThreads);
       if (n < end) {
-      while (ri + 1 < nr && rt->n0[ri + 1] <= n) ++ri;
-      const int64_t k = n - rt->n0[ri];
-      double t, a;
-      if (rt->single[ri]) {
-        t = rt->tin0[ri];
-        a = rt->acc0[ri];
-      } else {
-        t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
-        a = mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]);
-      }
-      const double* cs = cf + (rt->seg[ri] * D) * N;
-      for (int d = 0; d < D; ++d) {
-        double v = 0.0;
-        if (derivative < N) {
-          const double* c = cs + d * N;
-          v = row[N - 1] * c[N - 1];
+        while (ri + 1 < nr && rt->n0[ri + 1] <= n) ++ri;
+        const int64_t k = n - rt->n0[ri];
+        double t, a;
+        if (rt->single[ri]) {
+          t = rt->tin0[ri];
+          a = rt->acc0[ri];
+        } else {
+          t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
+          a = mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]);
+        }
+        const double* cs = cf + (rt->seg[ri] * D) * N;
+        for (int d = 0; d < D; ++d) {
+          double v = 0.0;
+          if (derivative < N) {
+            const double* c = cs + d * N;
+            v = c[N - 1];
 #pragma unroll
-          for (int j = N - 2; j >= 0; --j) {
-            if (j >= derivative) {
-              v = v * t;
-              v = v + row[j] * c[j];
+            for (int j = N - 2; j >= 0; --j) {
+              if (DER >= 0 ? j >= DER : j >= derivative) {
+                v = v * t;
+                v = v + c[j];
+              }
             }
           }
+          ob[lane * D + d] = v;
         }
-        ob[lane * D + d] = v;
-      }
-      if (sample_times) sample_times[base + n] = a;
+        if (sample_times) sample_times[base + n] = a;
       }
       __syncthreads();
       // the block's rows are contiguous in out: write them with consecutive lanes
@@ -343,10 +345,19 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   if (B == 0) return hipSuccess;
   const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-#define MTG_EVAL_CASE(NN)                                                                               \
-  case NN:                                                                                              \
-    launch_kernel(eval_range_kernel<NN>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, \
-                       coeffs, times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times);     \
+#define MTG_EVAL_LAUNCH(NN, DD)                                                                          \
+  launch_kernel(eval_range_kernel<NN, DD>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, coeffs, \
+                times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times)
+#define MTG_EVAL_CASE(NN)                 \
+  case NN:                                \
+    switch (derivative) {                 \
+      case 0: MTG_EVAL_LAUNCH(NN, 0); break; \
+      case 1: MTG_EVAL_LAUNCH(NN, 1); break; \
+      case 2: MTG_EVAL_LAUNCH(NN, 2); break; \
+      case 3: MTG_EVAL_LAUNCH(NN, 3); break; \
+      case 4: MTG_EVAL_LAUNCH(NN, 4); break; \
+      default: MTG_EVAL_LAUNCH(NN, -1); break; \
+    }                                     \
     break;
   switch (N) {
     MTG_EVAL_CASE(2)
@@ -358,6 +369,7 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
     default: return hipErrorInvalidValue;
   }
 #undef MTG_EVAL_CASE
+#undef MTG_EVAL_LAUNCH
   return hipGetLastError();
 }
 
