@@ -609,9 +609,13 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
     if (!out) {
       MTG_HIP_TRY(ctx, mtg::launch_eval_count(N, D, K, batch, times, t_start, t_end, dt, counts, ctx->stream));
     } else {
-      MTG_HIP_TRY(ctx, time_begin(ctx));
+      int cap = 0;
+      const size_t wsb = mtg::eval_workspace_bytes(K, batch, &cap);
+      MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(wsb, 256)));
+      MTG_HIP_TRY(ctx, time_begin(ctx, false));  // two kernels: the run table, then the samples
       MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative,
-                                              counts, offsets, out, sample_times, ctx->stream));
+                                              counts, offsets, out, sample_times, ctx->workspace, cap,
+                                              ctx->stream));
       MTG_HIP_TRY(ctx, time_end(ctx));
     }
     if (!(flags & MTG_FLAG_ASYNC)) MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -645,14 +649,17 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coeffs, coeffs, b_coeffs, hipMemcpyHostToDevice, ctx->stream));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_offsets, offsets, b_counts, hipMemcpyHostToDevice, ctx->stream));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_counts, counts, b_counts, hipMemcpyHostToDevice, ctx->stream));
-    MTG_HIP_TRY(ctx, time_begin(ctx));
+    int cap = 0;
+    const size_t wsb = mtg::eval_workspace_bytes(K, batch, &cap);
+    MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(wsb, 256)));
+    MTG_HIP_TRY(ctx, time_begin(ctx, false));
     MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<double*>(base + o_coeffs),
                                             reinterpret_cast<double*>(base + o_times), t_start, t_end, dt,
                                             derivative, reinterpret_cast<int64_t*>(base + o_counts),
                                             reinterpret_cast<int64_t*>(base + o_offsets),
                                             reinterpret_cast<double*>(base + o_out),
                                             sample_times ? reinterpret_cast<double*>(base + o_st) : nullptr,
-                                            ctx->stream));
+                                            ctx->workspace, cap, ctx->stream));
     MTG_HIP_TRY(ctx, time_end(ctx));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(out, base + o_out, b_out, hipMemcpyDeviceToHost, ctx->stream));
     if (sample_times) MTG_HIP_TRY(ctx, hipMemcpyAsync(sample_times, base + o_st, b_st, hipMemcpyDeviceToHost, ctx->stream));

@@ -216,7 +216,61 @@ __global__ void eval_count_kernel(int K, int64_t B, const double* times, double 
   counts[b] = ck.n;
 }
 
-// Runs per round of the LDS table (built by lane 0, consumed by the wave).
+// A run as stored in the HBM run table (eval_runs_kernel -> eval_range_kernel), 80 B.
+struct RunRec {
+  int64_t n0, L, tm, ti, am, ai;
+  double tin0, acc0;
+  int32_t tE, aE, seg, single;
+};
+
+// Per trajectory: how many runs the table holds and, when the clock had not stopped by then, its
+// state after them (the eval wave resumes the clock there).
+struct RunHead {
+  int64_t nruns, n;
+  double acc, tin, Ti;
+  int32_t seg, done;
+};
+
+// The clock, one thread per trajectory, writing its first `cap` runs to the run table.  The clock
+// is a serial chain per trajectory; run here, 64 trajectories share a wave's lanes, where the eval
+// kernel's lane 0 would run it alone while its wave waits.
+__global__ void eval_runs_kernel(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
+                                 int cap, RunHead* heads, RunRec* runs) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  Clock ck;
+  ck.init(times + b * K, K, t_start, t_end, dt);
+  RunRec* rr = runs + b * (int64_t)cap;
+  int64_t nr = 0;
+  Run r;
+  while (nr < cap && ck.next(&r)) {
+    RunRec w;
+    w.n0 = r.n0;
+    w.L = r.L;
+    w.tm = r.t.m;
+    w.ti = r.t.inc;
+    w.am = r.a.m;
+    w.ai = r.a.inc;
+    w.tin0 = r.tin0;
+    w.acc0 = r.acc0;
+    w.tE = r.t.E;
+    w.aE = r.a.E;
+    w.seg = r.seg;
+    w.single = r.single;
+    rr[nr++] = w;
+  }
+  RunHead h;
+  h.nruns = nr;
+  h.n = ck.n;
+  h.acc = ck.acc;
+  h.tin = ck.tin;
+  h.Ti = ck.Ti;
+  h.seg = ck.seg;
+  h.done = ck.done;
+  heads[b] = h;
+}
+
+// Runs per round of the LDS table (from the run table, or built by lane 0), consumed by the wave.
 constexpr int kRuns = 64;
 constexpr int kEvalThreads = 64;
 
@@ -235,7 +289,8 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
-                                                                  double* sample_times) {
+                                                                  double* sample_times, int cap,
+                                                                  const RunHead* heads, const RunRec* runs) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
   // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
 #pragma clang fp contract(off)
@@ -255,11 +310,50 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
   for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = base_coeff(derivative, i % N) * cb[i];
   const int64_t base = offsets[b];
   Clock ck;
-  if (lane == 0) ck.init(times + b * K, K, t_start, t_end, dt);
+  int64_t stored = 0, next_run = 0;  // runs in the HBM table, runs taken from it
+  const RunRec* rr = runs ? runs + b * (int64_t)cap : nullptr;
+  if (heads) {
+    const RunHead h = heads[b];
+    stored = h.nruns;
+    if (lane == 0) {  // resume the clock after the stored runs
+      ck.T = times + b * K;
+      ck.K = K;
+      ck.dt = dt;
+      ck.t_end = t_end;
+      ck.acc = h.acc;
+      ck.tin = h.tin;
+      ck.Ti = h.Ti;
+      ck.seg = h.seg;
+      ck.n = h.n;
+      ck.done = h.done != 0;
+    }
+  } else if (lane == 0) {
+    ck.init(times + b * K, K, t_start, t_end, dt);
+  }
   __shared__ int s_nr;
   __shared__ int64_t s_end;
   for (;;) {
-    if (lane == 0) {
+    if (next_run < stored) {  // a round from the run table: one run per lane
+      const int nr = (int)(stored - next_run < kRuns ? stored - next_run : kRuns);
+      if (lane < nr) {
+        const RunRec w = rr[next_run + lane];
+        rt->n0[lane] = w.n0;
+        rt->L[lane] = w.L;
+        rt->tm[lane] = w.tm;
+        rt->ti[lane] = w.ti;
+        rt->tE[lane] = w.tE;
+        rt->am[lane] = w.am;
+        rt->ai[lane] = w.ai;
+        rt->aE[lane] = w.aE;
+        rt->tin0[lane] = w.tin0;
+        rt->acc0[lane] = w.acc0;
+        rt->seg[lane] = w.seg;
+        rt->single[lane] = w.single;
+        if (lane == nr - 1) s_end = w.n0 + w.L;
+      }
+      if (lane == 0) s_nr = nr;
+      next_run += nr;
+    } else if (lane == 0) {
       int nr = 0;
       Run r;
       while (nr < kRuns && ck.next(&r)) {
@@ -339,15 +433,36 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
   return hipGetLastError();
 }
 
+size_t eval_workspace_bytes(int K, int64_t B, int* cap) {
+  // up to 128 runs per trajectory (config 2 has ~100), fewer for huge batches: the table is ~4% of
+  // the samples it describes at 128 and is capped at 2 GB; a trajectory with more runs than the
+  // table holds continues on its eval wave's lane 0
+  (void)K;
+  int c = 128;
+  while (c > 8 && (double)B * (c * sizeof(RunRec) + sizeof(RunHead)) > 2.0e9) c /= 2;
+  *cap = c;
+  return (size_t)B * (sizeof(RunHead) + (size_t)c * sizeof(RunRec));
+}
+
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs, const double* times,
                              double t_start, double t_end, double dt, int derivative, const int64_t* counts,
-                             const int64_t* offsets, double* out, double* sample_times, hipStream_t stream) {
+                             const int64_t* offsets, double* out, double* sample_times, void* ws, int cap,
+                             hipStream_t stream) {
   if (B == 0) return hipSuccess;
+  RunHead* heads = nullptr;
+  RunRec* runs = nullptr;
+  if (ws && cap > 0) {
+    heads = static_cast<RunHead*>(ws);
+    runs = reinterpret_cast<RunRec*>(heads + B);
+    const int block = 64;
+    launch_kernel(eval_runs_kernel, dim3((unsigned)((B + block - 1) / block)), dim3(block), 0, stream, K, B, times,
+                  t_start, t_end, dt, cap, heads, runs);
+  }
   const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
 #define MTG_EVAL_LAUNCH(NN, DD)                                                                          \
   launch_kernel(eval_range_kernel<NN, DD>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, coeffs, \
-                times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times)
+                times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs)
 #define MTG_EVAL_CASE(NN)                 \
   case NN:                                \
     switch (derivative) {                 \

@@ -88,9 +88,11 @@ hipError_t launch_min_max_magnitude(int N, const double* coeffs, const double* t
 // evaluateRange
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
                              double t_end, double dt, int64_t* counts, hipStream_t stream);
+// run-table workspace of launch_eval_range (bytes; *cap = runs stored per trajectory)
+size_t eval_workspace_bytes(int K, int64_t B, int* cap);
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs,
                              const double* times, double t_start, double t_end, double dt,
                              int derivative, const int64_t* counts, const int64_t* offsets, double* out,
-                             double* sample_times, hipStream_t stream);
+                             double* sample_times, void* ws, int cap, hipStream_t stream);
 
 }  // namespace mtg
