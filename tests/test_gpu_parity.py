@@ -452,3 +452,20 @@ def test_sharded_solves_bitwise_equal(gpu_ctx):
         b = gpu_ctx.solve_linear_batch(10, 4, vals[cut:], mask[cut:], times[cut:], cost=True)
         np.testing.assert_array_equal(np.concatenate([a["coeffs"], b["coeffs"]]), whole["coeffs"])
         np.testing.assert_array_equal(np.concatenate([a["cost"], b["cost"]]), whole["cost"])
+
+
+def test_evaluate_range_long_clock_vs_oracle(gpu_ctx):
+    """evaluateRange past the 128-run table (K = 30: ~300 runs, the rest resumed on the eval wave)
+    and derivative orders outside the compile-time set (5, 7): bit-exact with the oracle."""
+    O = _oracle()
+    B = 4
+    vals, mask, times = _bench_batch(B, seed0=23, K=30)
+    coeffs = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times)["coeffs"]
+    for deriv in (0, 5, 7):
+        out, st, counts, offs = gpu_ctx.evaluate_range_batch(coeffs, times, 0.0, 1e9, 0.01, deriv)
+        assert counts.min() > 0
+        for b in range(B):
+            ro, rst, n = O.evaluate_range(coeffs[b], times[b], 0.0, 1e9, 0.01, deriv, max_samples=int(counts[b]) + 10)
+            assert n == counts[b]
+            np.testing.assert_array_equal(st[offs[b]:offs[b] + n], rst)
+            np.testing.assert_array_equal(out[offs[b]:offs[b] + n], ro)
