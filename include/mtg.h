@@ -206,8 +206,9 @@ int mtg_min_max_magnitude_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch
 /* Timing of the most recent kernel launch(es) of this context on its stream
  * (hipEvent pair around the solve kernel), in milliseconds. */
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);
-/* Keep a HIP event pair per launch for the last `ring` launches (ring >= 1;
- * the default is 1).  mtg_kernel_times synchronizes on the newest event and
+/* Keep a HIP event pair per launch for the last `ring` launches (ring >= 0;
+ * the default is 1; 0 records no events).  Single-kernel calls carry the pair in
+ * the kernel's dispatch packet.  mtg_kernel_times synchronizes on the newest event and
  * writes up to n durations (ms, oldest first) of the launches still in the
  * ring; *n_out receives the count. */
 int mtg_enable_timing(mtg_ctx* ctx, int ring);

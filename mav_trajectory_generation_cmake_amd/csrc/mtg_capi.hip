@@ -77,9 +77,10 @@ hipError_t ensure(void** buf, size_t* have, size_t need) {
 // mtg::launch_kernel, which carries the event pair in its dispatch packet; otherwise (the split
 // path's two kernels) the events are recorded as stream markers around the launches.
 hipError_t time_begin(mtg_ctx* ctx, bool single = true) {
-  const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
   mtg::PendingEvents& pe = mtg::pending_events();
   pe = mtg::PendingEvents{};
+  if (ctx->ev_start.empty()) return hipSuccess;  // timing disabled (mtg_enable_timing(ctx, 0))
+  const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
   if (single) {
     pe.start = ctx->ev_start[slot];
     pe.stop = ctx->ev_stop[slot];
@@ -89,6 +90,7 @@ hipError_t time_begin(mtg_ctx* ctx, bool single = true) {
 }
 
 hipError_t time_end(mtg_ctx* ctx) {
+  if (ctx->ev_start.empty()) return hipSuccess;
   const size_t slot = (size_t)(ctx->launches % (int64_t)ctx->ev_start.size());
   mtg::PendingEvents& pe = mtg::pending_events();
   hipError_t e = hipSuccess;
@@ -677,7 +679,7 @@ int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms) {
 }
 
 int mtg_enable_timing(mtg_ctx* ctx, int ring) {
-  if (!ctx || ring < 1) return MTG_ERR_INVALID_ARGUMENT;
+  if (!ctx || ring < 0) return MTG_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> g(ctx->mu);
   MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
   MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
