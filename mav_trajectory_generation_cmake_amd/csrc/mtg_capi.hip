@@ -22,6 +22,8 @@ struct mtg_ctx {
   size_t staging_bytes = 0;
   void* workspace = nullptr;
   size_t workspace_bytes = 0;
+  void* pinned = nullptr;  // host mirror of the staging layout for small calls (hipHostMalloc)
+  size_t pinned_bytes = 0;
   // ring of (start, stop) events around kernel launches; launches counts recorded launches
   std::vector<hipEvent_t> ev_start, ev_stop;
   int64_t launches = 0;
@@ -59,6 +61,9 @@ int set_error(mtg_ctx* ctx, int code, const char* what) {
   } while (0)
 
 size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// host-pointer calls whose staged arrays fit this size go through one pinned buffer
+constexpr size_t kPinnedMax = 1u << 20;
 
 hipError_t ensure(void** buf, size_t* have, size_t need) {
   if (*have >= need) return hipSuccess;
@@ -170,7 +175,8 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   const size_t b_status = status ? sizeof(int32_t) * (size_t)pairs : 0;
   char* base = nullptr;
   size_t o_vals = 0, o_mask = 0, o_times = 0, o_scales = 0, o_coeffs = 0, o_free = 0, o_nfree = 0,
-         o_cost = 0, o_status = 0;
+         o_cost = 0, o_status = 0, out_end = 0;
+  bool pin = false;
   if (dev) {
     a.values = values;
     a.mask = mask;
@@ -194,11 +200,32 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     o_status = off; off = align_up(off + b_status);
     MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(off, 256)));
     base = static_cast<char*>(ctx->staging);
-    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_vals, values, b_vals, hipMemcpyHostToDevice, ctx->stream));
-    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_mask, mask, b_mask, hipMemcpyHostToDevice, ctx->stream));
-    MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
-    if (scales)
-      MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_scales, scales, b_scales, hipMemcpyHostToDevice, ctx->stream));
+    pin = off <= kPinnedMax;
+    if (pin) {
+      // small call (a drop-in PolynomialOptimization::solveLinear): pack the inputs into a pinned
+      // mirror of the staging layout and move them with ONE DMA each way, instead of one pageable
+      // copy per array (each of which the runtime bounces through its own pinned buffer)
+      if (ctx->pinned_bytes < off) {
+        if (ctx->pinned) MTG_HIP_TRY(ctx, hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        MTG_HIP_TRY(ctx, hipHostMalloc(&ctx->pinned, kPinnedMax, hipHostMallocDefault));
+        ctx->pinned_bytes = kPinnedMax;
+      }
+      char* hp = static_cast<char*>(ctx->pinned);
+      std::memcpy(hp + o_vals, values, b_vals);
+      std::memcpy(hp + o_mask, mask, b_mask);
+      std::memcpy(hp + o_times, times, b_times);
+      if (scales) std::memcpy(hp + o_scales, scales, b_scales);
+      MTG_HIP_TRY(ctx, hipMemcpyAsync(base, hp, o_coeffs, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_vals, values, b_vals, hipMemcpyHostToDevice, ctx->stream));
+      MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_mask, mask, b_mask, hipMemcpyHostToDevice, ctx->stream));
+      MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+      if (scales)
+        MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_scales, scales, b_scales, hipMemcpyHostToDevice, ctx->stream));
+    }
+    out_end = off;
     a.values = reinterpret_cast<const double*>(base + o_vals);
     a.mask = reinterpret_cast<const uint8_t*>(base + o_mask);
     a.times = reinterpret_cast<const double*>(base + o_times);
@@ -222,7 +249,17 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, (flags & MTG_FLAG_GENERAL_KERNEL) != 0));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
-  if (!dev) {
+  if (pin) {
+    char* hp = static_cast<char*>(ctx->pinned);
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(hp + o_coeffs, base + o_coeffs, out_end - o_coeffs, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (coeffs) std::memcpy(coeffs, hp + o_coeffs, b_coeffs);
+    if (free_out) std::memcpy(free_out, hp + o_free, b_free);
+    if (n_free_out) std::memcpy(n_free_out, hp + o_nfree, b_nfree);
+    if (cost_out) std::memcpy(cost_out, hp + o_cost, b_cost);
+    if (status) std::memcpy(status, hp + o_status, b_status);
+  } else if (!dev) {
     if (coeffs) MTG_HIP_TRY(ctx, hipMemcpyAsync(coeffs, base + o_coeffs, b_coeffs, hipMemcpyDeviceToHost, ctx->stream));
     if (free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(free_out, base + o_free, b_free, hipMemcpyDeviceToHost, ctx->stream));
     if (n_free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(n_free_out, base + o_nfree, b_nfree, hipMemcpyDeviceToHost, ctx->stream));
@@ -297,6 +334,7 @@ int mtg_destroy(mtg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->staging) (void)hipFree(ctx->staging);
   if (ctx->workspace) (void)hipFree(ctx->workspace);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   destroy_events(ctx);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
