@@ -203,7 +203,7 @@ def main():
         step_t = ctx_t.solve_call(N, r, v_d, m_d, t_d, out_d, split=args.split, general=args.general_kernel)
         if args.split:
             kname = "assemble+block_cholesky"
-        elif args.general_kernel or K > 12 or (N == 12 and K > 8):
+        elif args.general_kernel or K > 20 or (K > 12 and N != 12) or (N == 12 and 8 < K <= 12):
             kname = "solve_fused_kernel"
         else:
             kname = "solve_reg_kernel"

@@ -14,8 +14,10 @@ hipError_t launch_solve_reg_n12(const SolveArgs&, int, size_t, hipStream_t);
 
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes) {
   const int H = N / 2;
-  // G_v columns take H * KMAX doubles per lane: beyond ~50 the kernel spills (N=12, K > 8)
-  if (reg_kmax(K) < 0 || H * reg_kmax(K) > 50) return false;
+  // G_v columns take H * KMAX doubles per lane: beyond ~50 the 2-waves-per-SIMD kernel spills
+  // (N=12, K > 8); the wide bucket (N = 12, K <= 20) runs at 1 wave per SIMD instead
+  const int km = reg_kmax(K);
+  if (km < 0 || (H * km > 50 && !(N == 12 && km == kRegKMaxWide))) return false;
   int lg = 8;
   while (lg < H + D) lg *= 2;
   if (lg > 64) return false;
