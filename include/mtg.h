@@ -70,7 +70,8 @@ extern "C" {
 #define MTG_FLAG_ASYNC 2u              /* do not synchronize the stream before returning */
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
 #define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
-                                          (default: the register-resident kernel when K <= 12) */
+                                          (default: the register-resident kernel when K <= 12, and
+                                          for N = 12 when K <= 20) */
 
 typedef struct mtg_ctx mtg_ctx;
 

@@ -1,5 +1,5 @@
 // mtg_device.h -- device helpers shared by the solve kernels (mtg_kernels.hip: general
-// LDS-resident kernel; mtg_solve_reg.hip: register-resident kernel for K <= 12).
+// LDS-resident kernel; mtg_solve_reg.hip: register-resident kernel for K <= 12, N = 12 to K = 20).
 #pragma once
 
 #include <float.h>

@@ -52,7 +52,8 @@ struct SolveArgs {
 bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes, int* traj_per_block);
 
 // Launch the fused solve on `stream`: the register-resident kernel (mtg_solve_reg.hip) when the
-// shape allows it (K <= 12, LDS slot fits) and `general` is false, else the general LDS-resident
+// shape allows it (reg_geometry: K <= 12, or N = 12 with K <= 20; LDS slot fits) and `general` is
+// false, else the general LDS-resident
 // kernel (mtg_kernels.hip).
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, bool general = false);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);

@@ -18,7 +18,7 @@ TRUTH_TOL = 1e-9
 ORACLE_TOL_N10 = 1e-6
 
 # the three solve paths behind mtg_solve_linear_batch: the default (register-resident kernel for
-# K <= 12, else the general one), the general LDS-resident fused kernel, and the two-kernel split path
+# K <= 12 and for N = 12 up to K = 20, else the general one), the general LDS-resident fused kernel, and the two-kernel split path
 PATHS = {"default": {}, "general": {"general": True}, "split": {"split": True}}
 
 
