@@ -236,6 +236,15 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     a.cost_out = cost_out ? reinterpret_cast<double*>(base + o_cost) : nullptr;
     a.status = status ? reinterpret_cast<int32_t*>(base + o_status) : nullptr;
   }
+  // From here on a failure must not return while a DMA may still read ctx->pinned (the next call
+  // would overwrite it): the pinned path drains the stream before reporting any error.
+  struct PinnedDrain {
+    mtg_ctx* ctx;
+    bool armed;
+    ~PinnedDrain() {
+      if (armed) (void)hipStreamSynchronize(ctx->stream);
+    }
+  } drain{ctx, pin};
   if (free_out && b_free) {
     // entries beyond n_free are left zero
     MTG_HIP_TRY(ctx, hipMemsetAsync(const_cast<double*>(a.free_out), 0, b_free, ctx->stream));
@@ -259,6 +268,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     if (n_free_out) std::memcpy(n_free_out, hp + o_nfree, b_nfree);
     if (cost_out) std::memcpy(cost_out, hp + o_cost, b_cost);
     if (status) std::memcpy(status, hp + o_status, b_status);
+    drain.armed = false;
   } else if (!dev) {
     if (coeffs) MTG_HIP_TRY(ctx, hipMemcpyAsync(coeffs, base + o_coeffs, b_coeffs, hipMemcpyDeviceToHost, ctx->stream));
     if (free_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(free_out, base + o_free, b_free, hipMemcpyDeviceToHost, ctx->stream));

@@ -15,11 +15,14 @@ hipError_t launch_solve_reg_n12(const SolveArgs&, int, size_t, hipStream_t);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes) {
   const int H = N / 2;
   // G_v columns take H * KMAX doubles per lane: beyond ~50 the 2-waves-per-SIMD kernel spills
-  // (N=12, K > 8); the wide bucket (N = 12, K <= 20) runs at 1 wave per SIMD instead
+  // (N=12, K > 8); the wide bucket (N = 12, K <= 20) splits G over two lane sets instead
   const int km = reg_kmax(K);
   if (km < 0 || (H * km > 50 && !(N == 12 && km == kRegKMaxWide))) return false;
   int lg = 8;
   while (lg < H + D) lg *= 2;
+  // the wide bucket parks G_v, v >= KMAX/2, on lanes 9..14 of the trajectory's group: it needs a
+  // 16-lane group even when H + D <= 8 (N = 12 with D = 1 or 2)
+  if (N == 12 && km == kRegKMaxWide && lg < kRegWideMinLanes) lg = kRegWideMinLanes;
   if (lg > 64) return false;
   const size_t bytes = (size_t)reg_lds_doubles(N, D, K, lg) * sizeof(double);
   if (bytes > kMaxLdsPerBlock) return false;

@@ -240,6 +240,35 @@ def test_wide_register_bucket_n12(gpu_ctx, K):
     assert scale_normalised_error(d["coeffs"], g["coeffs"], rt) <= 1e-9
 
 
+@pytest.mark.parametrize("K", [13, 20])
+@pytest.mark.parametrize("D", [1, 2, 3, 4, 6, 11])
+def test_wide_register_bucket_n12_dimensions(gpu_ctx, D, K):
+    """The wide bucket parks G_v, v >= 10, on lanes 9..14 of each trajectory's lane group, so the
+    group needs 16 lanes even where H + D <= 8 (D = 1, 2: a yaw or planar problem), and for
+    D >= 4 those lanes are dimension lanes too; D = 11 takes a 32-lane group.  Against the general
+    LDS-resident kernel (1e-9) and the oracle, with waypoint masks and with mixed masks."""
+    O = _oracle()
+    B = 21
+    vals, mask, times = _bench_batch_d(B, D, seed0=900 + D, K=K, N=12)
+    rng = np.random.default_rng(D * 100 + K)
+    mixed = mask.copy()
+    mixed[:, 1:-1] |= (rng.integers(0, 2, size=mixed[:, 1:-1].shape) * 0x06).astype(np.uint8)
+    for m in (mask, mixed):
+        d = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True)
+        g = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True, general=True)
+        assert np.all(d["status"] == 0) and np.all(g["status"] == 0)
+        assert scale_normalised_error(d["coeffs"], g["coeffs"], times) <= 1e-9, (D, K)
+        np.testing.assert_allclose(d["cost"], g["cost"], rtol=1e-9)
+        ref = O.solve_linear_batch(12, 3, vals, m.astype(np.uint32), times)
+        assert scale_normalised_error(d["coeffs"], ref, times) <= 1e-3
+        assert check_path(vals, m, times, d["coeffs"], 12, relative=True) < 1e-6
+
+
+def _bench_batch_d(B, D, seed0=0, K=10, N=10):
+    from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
+    return random_vertices_path_batch(N, D, K, B, seed0=seed0)
+
+
 @pytest.mark.parametrize("path", ["default", "split"])
 def test_time_sweep_matches_solves(gpu_ctx, path):
     """mtg_time_sweep_batch == computeCost of separate solves at scaled times."""
