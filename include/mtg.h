@@ -1,14 +1,15 @@
 /*
  * mtg.h -- C ABI of the MI355X batched minimum-derivative polynomial
- * optimizer (libmtg.so).  Plain C types only: pointers, sizes, status codes.
+ * optimizer (libmav_trajectory_generation.so).  Plain C types only: pointers, sizes, status codes.
  *
  * The reference (magrimm/mav_trajectory_generation_cmake) has no FFI; its
  * boundary is the C++ template class PolynomialOptimization<N>
  * (mav_trajectory_generation/include/mav_trajectory_generation/
  * polynomial_optimization_linear.h:45-269).  Each entry point below states
- * which reference interface it replaces.  The C++ drop-in classes in
- * include/mav_trajectory_generation/ are written on top of this ABI, and
- * INTEGRATION.md shows the bindings (C++, ctypes) a maintainer would add.
+ * which reference interface it replaces.  The C++ drop-in headers at the
+ * reference's include paths (include/mav_trajectory_generation/ headers, namespace
+ * mav_trajectory_generation) are written on top of this ABI, and
+ * INTEGRATION.md shows the bindings (C++, CMake, ctypes) a maintainer adds.
  *
  * Rules: the library never aborts and never throws; calls return MTG_OK or a
  * negative MTG_ERR_*.  All buffers are caller-owned and never retained after
@@ -215,6 +216,18 @@ int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms);
 int mtg_enable_timing(mtg_ctx* ctx, int ring);
 int mtg_kernel_times(mtg_ctx* ctx, float* ms, int n, int* n_out);
 
+/* Host (CPU) path of mtg_solve_linear_batch, no context and no GPU needed: the same algorithm
+ * as the HIP kernels (exact tables, symmetric pinning, block LDL^T Thomas), in scalar C++ on the
+ * calling thread(s).  For one problem it is the lowest-latency path (a GPU round trip costs more
+ * than the solve itself): the C++ drop-in PolynomialOptimization<N>::solveLinear uses it by
+ * default (BASELINE config 1), replacing the reference's CPU solveLinear (lin_impl:329-369).
+ * Same arrays and per-trajectory status as mtg_solve_linear_batch, all host pointers;
+ * threads <= 0: one per hardware thread. */
+int mtg_host_solve_linear_batch(int N, int D, int K, int derivative_to_optimize, int64_t batch,
+                                const double* values, const uint8_t* fixed_mask, const double* times,
+                                double* coeffs, double* free_out, int32_t* n_free_out, double* cost_out,
+                                int32_t* status, int threads);
+
 /* ---- Host utilities (no GPU): the reference's synthetic-input generators,
  * bit-exact with libstdc++ <random>, packed straight into the ABI layout.
  * Trajectory b of a batch uses seed (seed0 + b).  values [B][V][h][D],
@@ -233,6 +246,30 @@ int mtg_host_random_vertices_path_batch(int N, int D, int K, double average_dist
                                         double v_max, double a_max, double magic_fabian_constant,
                                         double* values, uint8_t* fixed_mask, double* times,
                                         int threads);
+
+/* estimateSegmentTimes (src/vertex.cpp:162-178) on explicit positions [n_vertices][D]:
+ * times[i] = 2 d / v_max (1 + magic v_max / a_max exp(-2 d / v_max)), d = |p_{i+1} - p_i| with
+ * Eigen's norm reduction order.  times [n_vertices - 1]. */
+int mtg_host_estimate_segment_times(int n_vertices, int D, const double* positions, double v_max, double a_max,
+                                    double magic_fabian_constant, double* times);
+
+/* Per-segment matrices of PolynomialOptimization<N> at segment time T (> 0), N x N row-major, any
+ * pointer may be NULL:
+ *   A      setupMappingMatrix (lin_impl:102-111)
+ *   A_inv  A(T)^-1 (invertMappingMatrix, lin_impl:133-169), from the exact A(1)^-1 table:
+ *          diag(T^-j) A(1)^-1 S(T), S = diag(T^(slot mod N/2))
+ *   Q      computeQuadraticCostJacobian(derivative_to_optimize, T) (lin_impl:574-589)
+ *   H      A^-T Q A^-1 (constructR's per-segment block, lin_impl:305-308), from the exact table:
+ *          T^(1-2r) S Htilde S
+ * They back getA / getAInverse / getR of the C++ drop-in. */
+int mtg_host_segment_matrices(int N, int derivative_to_optimize, double T, double* A, double* A_inv, double* Q,
+                              double* H);
+
+/* Host form of mtg_coefficients_from_vertices_batch (setFreeConstraints +
+ * updateSegmentsFromCompactConstraints, lin_impl:253-273) for the C++ drop-in's single problems:
+ * vertex_values [B][V][h][D] (all derivatives), times [B][K] -> coeffs [B][K][D][N]. */
+int mtg_host_coefficients_from_vertices_batch(int N, int D, int K, int64_t batch, const double* vertex_values,
+                                              const double* times, double* coeffs, int threads);
 
 #ifdef __cplusplus
 }

@@ -3,14 +3,15 @@
 Drop-in for the linear solve path of magrimm/mav_trajectory_generation_cmake
 (PolynomialOptimization<N>::setupFromVertices + solveLinear, and
 Trajectory::evaluateRange).  The compute path is hand-written HIP for gfx950
-behind a C ABI (include/mtg.h, lib/libmtg.so); this package is a thin Python
+behind a C ABI (include/mtg.h, lib/libmav_trajectory_generation.so); this package is a thin Python
 host layer over that ABI.  See DESIGN.md.
 """
 from . import _native
 from ._native import MTGError, device_count, load
-from .solver import (Context, default_context, full_vertex_values, random_vertices_batch,
+from .solver import (Context, default_context, full_vertex_values, host_solve_linear_batch, random_vertices_batch,
                      random_vertices_path_batch, solve_linear_batch)
 
-__all__ = ["MTGError", "Context", "default_context", "device_count", "full_vertex_values", "load",
+__all__ = ["MTGError", "Context", "default_context", "device_count", "full_vertex_values", "host_solve_linear_batch",
+           "load",
            "random_vertices_batch",
            "random_vertices_path_batch", "solve_linear_batch", "_native"]

@@ -1,4 +1,4 @@
-"""ctypes binding of libmtg.so (include/mtg.h).
+"""ctypes binding of libmav_trajectory_generation.so (the C ABI, include/mtg.h).
 
 The product path has no CPU fallback: if the HIP library is missing or no GPU
 is visible, calls raise.  PyTorch is only used (in solver.py) as an optional
@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmtg.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libmav_trajectory_generation.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "mtg.h")
 
 MTG_OK = 0
@@ -72,6 +72,16 @@ _SIGNATURES = {
     "mtg_enable_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mtg_kernel_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_int)]),
+    "mtg_host_solve_linear_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
+                                                   _c_dp, _c_dp, ctypes.c_int]),
+    "mtg_host_estimate_segment_times": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_double,
+                                                       ctypes.c_double, ctypes.c_double, _c_dp]),
+    "mtg_host_segment_matrices": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_double, _c_dp, _c_dp,
+                                                 _c_dp, _c_dp]),
+    "mtg_host_coefficients_from_vertices_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                                 ctypes.c_int64, _c_dp, _c_dp, _c_dp,
+                                                                 ctypes.c_int]),
     "mtg_host_random_vertices_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                       _c_dp, _c_dp, ctypes.c_uint32, ctypes.c_int64,
                                                       ctypes.c_double, ctypes.c_double, ctypes.c_double,
@@ -110,11 +120,11 @@ def hip_runtimes_mapped():
 
 def _share_torch_runtime():
     """PyTorch-ROCm wheels bundle their own libamdhip64 (soname libamdhip64.so.7, the
-    same as /opt/rocm's).  Loading torch first makes the dynamic linker bind libmtg's
+    same as /opt/rocm's).  Loading torch first makes the dynamic linker bind the library's
     libamdhip64.so.7 dependency to torch's already-loaded copy, so the process has ONE
-    HIP runtime: torch stream handles and allocations are then valid in libmtg.  Loading
-    libmtg first would map /opt/rocm's runtime and torch would later map a second one,
-    whose streams/devices libmtg cannot see.  Set MTG_NO_TORCH=1 to skip (torch-free use)."""
+    HIP runtime: torch stream handles and allocations are then valid in the library.  Loading
+    the library first would map /opt/rocm's runtime and torch would later map a second one,
+    whose streams/devices the library cannot see.  Set MTG_NO_TORCH=1 to skip (torch-free use)."""
     if os.environ.get("MTG_NO_TORCH") == "1":
         return
     try:
@@ -124,13 +134,13 @@ def _share_torch_runtime():
 
 
 def load(path=None):
-    """Load libmtg.so; raises if it has not been built (no fallback)."""
+    """Load the library; raises if it has not been built (no fallback)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
     p = path or os.environ.get("MTG_LIBRARY", LIB_PATH)
     if not os.path.exists(p):
-        raise MTGError(MTG_ERR_NO_DEVICE, "libmtg.so not found at %s: run __graft_entry__.build()" % p)
+        raise MTGError(MTG_ERR_NO_DEVICE, "libmav_trajectory_generation.so not found at %s: run __graft_entry__.build()" % p)
     _share_torch_runtime()
     lib = ctypes.CDLL(p)
     for name, (res, args) in _SIGNATURES.items():

@@ -1,4 +1,4 @@
-// mtg_host.cpp -- host utilities of libmtg.so (no GPU): the reference's
+// mtg_host.cpp -- host utilities of libmav_trajectory_generation.so (no GPU): the reference's
 // synthetic problem generators, bit-exact with libstdc++ <random> because
 // they use it, packed straight into the ABI layout of include/mtg.h.
 //
@@ -201,3 +201,12 @@ int mtg_host_random_vertices_path_batch(int N, int D, int K, double average_dist
 }
 
 }  // extern "C"
+
+extern "C" int mtg_host_estimate_segment_times(int n_vertices, int D, const double* positions, double v_max,
+                                               double a_max, double magic_fabian_constant, double* times) {
+  if (n_vertices < 1 || D < 1 || !positions || (n_vertices > 1 && !times)) return MTG_ERR_INVALID_ARGUMENT;
+  Gen g(n_vertices, D, 1);
+  for (int v = 0; v < n_vertices; ++v) g.set(v, 0, positions + (size_t)v * D);
+  estimate_times(g, v_max, a_max, magic_fabian_constant, times);
+  return MTG_OK;
+}

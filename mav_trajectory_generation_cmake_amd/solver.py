@@ -1,4 +1,4 @@
-"""Batched solver API over the C ABI (libmtg.so).
+"""Batched solver API over the C ABI (libmav_trajectory_generation.so).
 
 Arrays may be numpy arrays (host; the library stages them through HBM) or
 torch CUDA tensors (device-resident; launched on torch's current stream so
@@ -380,6 +380,35 @@ def default_context(device=0):
 
 def solve_linear_batch(N, r, values, mask, times, device=0, **kw):
     return default_context(device).solve_linear_batch(N, r, values, mask, times, **kw)
+
+
+def host_solve_linear_batch(N, r, values, mask, times, free=False, n_free=False, cost=False, status=False,
+                            threads=1):
+    """The library's host (CPU) solve path (mtg_host_solve_linear_batch): same algorithm and outputs as
+    Context.solve_linear_batch, no GPU.  The drop-in PolynomialOptimization<N>::solveLinear uses it for
+    single problems (BASELINE config 1)."""
+    lib = nat.load()
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    B, V, h, D = values.shape
+    K = V - 1
+    assert h == N // 2, "values must be [B][K+1][N/2][D]"
+    assert mask.shape == (B, V) and times.shape == (B, K)
+    out = {"coeffs": np.empty((B, K, D, N))}
+    if free:
+        out["free"] = np.empty((B, D, V * h))
+    if n_free:
+        out["n_free"] = np.empty((B,), np.int32)
+    if cost:
+        out["cost"] = np.empty((B,))
+    if status:
+        out["status"] = np.empty((B,), np.int32)
+    nat.check(lib.mtg_host_solve_linear_batch(N, D, K, r, B, _addr(values), _addr(mask), _addr(times),
+                                              _addr(out["coeffs"]), _addr(out.get("free")),
+                                              _addr(out.get("n_free")), _addr(out.get("cost")),
+                                              _addr(out.get("status")), threads))
+    return out
 
 
 # ----------------------------------------------------------------- generators

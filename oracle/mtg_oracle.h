@@ -9,7 +9,7 @@
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
  * load this library, and only as the checker / the timed CPU baseline.  The
- * product path (libmtg.so) never links or calls it.
+ * product path (libmav_trajectory_generation.so) never links or calls it.
  *
  * Parity pinning (see DESIGN.md "Oracle"): the reference needs Eigen3, glog
  * and nlopt, none present, so it cannot be compiled here.  This restatement is

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase cycle stamps of time_jacobian_kernel (config 5; debug build: make -C ... timing).
 
-Run: MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmtg.so python scripts/jac_phase_timing.py
+Run: MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmav_trajectory_generation.so python scripts/jac_phase_timing.py
 Each wave's lane 0 writes its s_memtime stamps (entry, staged, W formed, sweep done, stored) over
 cost[b0][8 wave .. 8 wave + 4]; this prints the phase durations and the spread of entry times.
 """

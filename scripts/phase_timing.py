@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase cycle counts of the register-resident kernel (debug build: make -C ... timing).
 
-Run: MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmtg.so python scripts/phase_timing.py
+Run: MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmav_trajectory_generation.so python scripts/phase_timing.py
 """
 import os
 import sys

@@ -9,5 +9,5 @@ for B in 1024 4096 8192 10000 16384 32768 65536 131072; do
   python3 -c "import json; d=json.load(open('gpurun_out/sweep_$B.json')); r=d['roofline']; print('B=$B kern_ms=%.4f step_ms=%.4f frac=%.3f' % (r['kernel_ms'], d['ms_per_step'], r['frac']))"
 done
 for B in 8192 125000; do
-  B=$B MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmtg.so timeout -k 10 120 python scripts/phase_timing.py || exit $?
+  B=$B MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmav_trajectory_generation.so timeout -k 10 120 python scripts/phase_timing.py || exit $?
 done

@@ -24,7 +24,7 @@ def _has_gpu():
 def gpu_ctx():
     from mav_trajectory_generation_cmake_amd import Context
     if not _has_gpu():
-        pytest.fail("GPU test selected but no HIP device / libmtg.so is available")
+        pytest.fail("GPU test selected but no HIP device / libmav_trajectory_generation.so is available")
     ctx = Context(0)
     yield ctx
     ctx.close()

@@ -1,4 +1,4 @@
-"""CPU tests of the drop-in boundary (include/mtg.h <-> libmtg.so <-> _native.py).
+"""CPU tests of the drop-in boundary (include/mtg.h <-> libmav_trajectory_generation.so <-> _native.py).
 
 No compute calls here: these run without a GPU and check that the C ABI library
 loads, exports exactly what the header declares, validates arguments and
@@ -59,7 +59,7 @@ def test_status_strings():
 
 
 def test_one_hip_runtime_in_process():
-    """libmtg must bind to the same libamdhip64 as torch (see _native._share_torch_runtime)."""
+    """The library must bind to the same libamdhip64 as torch (see _native._share_torch_runtime)."""
     pytest.importorskip("torch")
     nat.load()
     assert len(nat.hip_runtimes_mapped()) == 1, nat.hip_runtimes_mapped()
@@ -92,7 +92,7 @@ def test_no_device_fails_loudly():
 
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(nat.MTGError):
-        nat.load(str(tmp_path / "libmtg.so"))
+        nat.load(str(tmp_path / "libmav_trajectory_generation.so"))
 
 
 def test_host_generator_argument_errors():
@@ -113,5 +113,5 @@ def test_cpp_header_compiles_with_c_compiler(tmp_path):
     exe = tmp_path / "t"
     libdir = os.path.dirname(nat.LIB_PATH)
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c), "-o",
-                    str(exe), "-L", libdir, "-lmtg", "-Wl,-rpath," + libdir], check=True)
+                    str(exe), "-L", libdir, "-lmav_trajectory_generation", "-Wl,-rpath," + libdir], check=True)
     assert subprocess.run([str(exe)]).returncode == 0

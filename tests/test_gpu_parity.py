@@ -114,7 +114,12 @@ def test_full_size_invariants(gpu_ctx):
     assert errs.max() <= 1e-4
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     from make_golden import truth_solve
-    for b in np.argsort(errs)[::-1][:3]:
+    # every trajectory where the kernel and the reference algorithm disagree by more than north_star's
+    # 1e-6 is arbitrated by 60-digit truth: the kernel must be within 1e-6 of truth or closer to it
+    # than the reference algorithm is (the worst one always, as a check of the arbitration itself)
+    arbitrate = sorted(set(np.nonzero(errs > ORACLE_TOL_N10)[0].tolist()) | {int(np.argmax(errs))})
+    assert len(arbitrate) <= 10, len(arbitrate)
+    for b in arbitrate:
         tr = truth_solve(10, 4, vals[b], mask[b], times[b])[0]
         e_gpu = scale_normalised_error(out["coeffs"][b:b + 1], tr[None], times[b:b + 1])
         e_ref = scale_normalised_error(ref[b:b + 1], tr[None], times[b:b + 1])
@@ -528,3 +533,34 @@ def test_evaluate_range_long_clock_vs_oracle(gpu_ctx):
             assert n == counts[b]
             np.testing.assert_array_equal(st[offs[b]:offs[b] + n], rst)
             np.testing.assert_array_equal(out[offs[b]:offs[b] + n], ro)
+
+
+@pytest.mark.parametrize("K", [2, 10, 13, 50])
+def test_host_path_matches_gpu(gpu_ctx, K):
+    """The library's host solve path (single problems of the drop-in) and the GPU kernels solve the
+    same system with the same tables: they agree far inside the parity tolerance."""
+    from mav_trajectory_generation_cmake_amd import host_solve_linear_batch
+    vals, mask, times = _bench_batch(64, seed0=4321, K=K)
+    h = host_solve_linear_batch(10, 4, vals, mask, times, free=True, cost=True, status=True)
+    g = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, free=True, cost=True, status=True)
+    np.testing.assert_array_equal(h["status"], g["status"])
+    assert scale_normalised_error(h["coeffs"], g["coeffs"], times) <= 1e-9
+    np.testing.assert_allclose(h["cost"], g["cost"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
+def test_not_spd_status(gpu_ctx, path):
+    """Segment times so large that T^k overflows: the pivots of R_pp are not finite, which the
+    kernels report as MTG_TRAJ_NOT_SPD (the reference's SparseQR would not notice, lin_impl:355-368)."""
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    vals, mask, times = _bench_batch(16, seed0=12)
+    times = times.copy()
+    times[3, :] = 1e200
+    times[7, :] = 1e150
+    out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True, **PATHS[path])
+    bad = {3, 7}
+    for b in range(16):
+        if b in bad:
+            assert out["status"][b] & nat.MTG_TRAJ_NOT_SPD, (b, out["status"][b])
+        else:
+            assert out["status"][b] == 0, (b, out["status"][b])

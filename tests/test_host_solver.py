@@ -1,0 +1,151 @@
+"""The library's host solve path (mtg_host_solve_linear_batch, csrc/mtg_host_solve.cpp): the same
+algorithm as the HIP kernels in scalar C++, used by the drop-in PolynomialOptimization<N> for
+single problems (BASELINE config 1, "on CPU").  CPU tests: against the 60-digit truth fixtures and
+the oracle (the restated reference algorithm), with the GPU parity tests' tolerances."""
+import numpy as np
+import pytest
+
+from _util import (check_path, golden_cases, load_golden, masked_elementwise_rel, scale_normalised_error,
+                   to_abi)
+
+import mav_trajectory_generation_cmake_amd as mtg
+from mav_trajectory_generation_cmake_amd import _native as nat
+
+TRUTH_TOL = 1e-9
+ORACLE_TOL_N10 = 1e-6
+
+
+def _oracle():
+    from oracle import pyoracle
+    return pyoracle
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_truth(case):
+    g = load_golden(case)
+    N, r = int(g["N"]), int(g["r"])
+    vals, mask = to_abi(g["values"], g["mask"], N)
+    out = mtg.host_solve_linear_batch(N, r, vals, mask, g["times"], free=True, n_free=True, cost=True, status=True)
+    assert np.all(out["status"] & 0xFF == 0), out["status"]
+    assert scale_normalised_error(out["coeffs"], g["coeffs"], g["times"]) <= TRUTH_TOL, case
+    assert masked_elementwise_rel(out["coeffs"], g["coeffs"], g["times"], floor=1e-4) <= 1e-6, case
+    np.testing.assert_array_equal(out["n_free"], g["n_free"])
+    assert np.max(np.abs(out["cost"] - g["cost"]) / np.maximum(np.abs(g["cost"]), 1e-300)) <= 1e-9
+    for b in range(len(out["n_free"])):
+        nf = int(g["n_free"][b])
+        if nf:
+            ref = g["free"][b][:, :nf]
+            scale = np.maximum(np.max(np.abs(ref), axis=1, keepdims=True), 1e-300)
+            assert np.max(np.abs(out["free"][b][:, :nf] - ref) / scale) <= 1e-7, case
+            assert np.all(out["free"][b][:, nf:] == 0.0)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 5, 9, 10, 12, 13, 20, 50, 100])
+def test_segment_counts_vs_oracle(K):
+    """The reference bench's K in {2, 10, 50, 100} (src/polynomial_timing_evaluation.cpp:117) and the
+    GPU kernels' bucket edges."""
+    O = _oracle()
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, K, 16, seed0=77)
+    out = mtg.host_solve_linear_batch(10, 4, vals, mask, times, status=True, cost=True)
+    assert np.all(out["status"] == 0)
+    ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
+    assert scale_normalised_error(out["coeffs"], ref, times) <= ORACLE_TOL_N10
+    assert check_path(vals, mask, times, out["coeffs"], 10, relative=True) < 1e-8
+
+
+def test_mixed_masks_vs_oracle():
+    """Per-problem masks with extra fixed derivatives at interior vertices (any pattern)."""
+    O = _oracle()
+    B = 64
+    vals, mask, times = mtg.random_vertices_batch(10, 3, 7, B, [-10, -20, -10], [10, 20, 10], seed0=9)
+    rng = np.random.default_rng(5)
+    mask = mask.copy()
+    mask[:, 1:-1] |= (rng.integers(0, 32, size=mask[:, 1:-1].shape) & 0x1E).astype(np.uint8)
+    vals = vals + rng.normal(size=vals.shape) * (mask[:, :, None, None] > 0)
+    out = mtg.host_solve_linear_batch(10, 4, vals, mask, times, status=True)
+    assert np.all(out["status"] == 0)
+    ref = O.solve_linear_batch(10, 4, vals, mask.astype(np.uint32), times)
+    assert scale_normalised_error(out["coeffs"], ref, times) <= ORACLE_TOL_N10
+    assert check_path(vals, mask, times, out["coeffs"], 10, relative=True) < 1e-8
+
+
+@pytest.mark.parametrize("N,D,r", [(4, 1, 1), (6, 2, 2), (8, 3, 3), (12, 4, 5), (12, 3, 0)])
+def test_other_shapes_vs_oracle(N, D, r):
+    O = _oracle()
+    vals, mask, times = mtg.random_vertices_batch(N, D, 6, 16, [-5.0] * D, [5.0] * D, seed0=31,
+                                                  max_derivative=N // 2 - 1)
+    out = mtg.host_solve_linear_batch(N, r, vals, mask, times, status=True)
+    assert np.all(out["status"] == 0)
+    assert check_path(vals, mask, times, out["coeffs"], N, relative=True) < 1e-7
+    if N <= 10:
+        ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
+        assert scale_normalised_error(out["coeffs"], ref, times) <= ORACLE_TOL_N10
+    else:
+        # N = 12: the FP64 reference algorithm itself is 1e-4 from truth here (r = 0: 1.6e-4 .. 5.6e-4
+        # on these problems), so the gate is 60-digit truth
+        import os
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+        from make_golden import truth_solve
+        for b in range(3):
+            tr = truth_solve(N, r, vals[b], mask[b], times[b])[0]
+            assert scale_normalised_error(out["coeffs"][b:b + 1], tr[None], times[b:b + 1]) <= TRUTH_TOL
+
+
+def test_status_bits():
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, 10, 6, seed0=4)
+    times = times.copy()
+    times[1, 3] = 0.0
+    times[2, 0] = -1.0
+    times[3, 5] = np.nan
+    times[4, :] = 1e200  # T^k overflows: the pivots of R_pp are not finite (MTG_TRAJ_NOT_SPD)
+    out = mtg.host_solve_linear_batch(10, 4, vals, mask, times, status=True)
+    assert out["status"][0] == 0 and out["status"][5] == 0
+    assert all(out["status"][i] & nat.MTG_TRAJ_BAD_TIME for i in (1, 2, 3))
+    assert out["status"][4] & nat.MTG_TRAJ_NOT_SPD
+    # orders > N/2-1 are dropped with a warning (lin_impl:74-95): same result as without them
+    v8, m8, t8 = mtg.random_vertices_path_batch(8, 3, 6, 8)
+    a = mtg.host_solve_linear_batch(8, 3, v8, m8, t8, status=True)
+    b = mtg.host_solve_linear_batch(8, 3, v8, m8 & 0x0F, t8, status=True)
+    assert np.all(a["status"] == nat.MTG_TRAJ_WARN_DROPPED) and np.all(b["status"] == 0)
+    np.testing.assert_array_equal(a["coeffs"], b["coeffs"])
+    with pytest.raises(nat.MTGError) as e:
+        mtg.host_solve_linear_batch(10, 5, vals, mask, times)
+    assert e.value.code == nat.MTG_ERR_BAD_DERIVATIVE
+
+
+def test_free_values_ignored_and_threads_bitwise():
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, 10, 300, seed0=8)
+    a = mtg.host_solve_linear_batch(10, 4, vals, mask, times, cost=True)
+    v2 = vals.copy()
+    for k in range(5):
+        v2[:, :, k, :][((mask >> k) & 1) == 0] = np.nan
+    b = mtg.host_solve_linear_batch(10, 4, v2, mask, times, cost=True, threads=4)
+    np.testing.assert_array_equal(a["coeffs"], b["coeffs"])
+    np.testing.assert_array_equal(a["cost"], b["cost"])
+
+
+def test_segment_matrices():
+    """mtg_host_segment_matrices: A is the reference's setupMappingMatrix, A^-1 inverts it, Q is
+    computeQuadraticCostJacobian, H = A^-T Q A^-1 (the oracle's FP64 restatements)."""
+    import ctypes
+    O = _oracle()
+    lib = nat.load()
+    for N, r in ((10, 4), (12, 3), (6, 0)):
+        for T in (0.013, 1.0, 3.7, 41.0):
+            A, Ai, Q, H = (np.zeros((N, N)) for _ in range(4))
+            assert lib.mtg_host_segment_matrices(N, r, T, A.ctypes.data, Ai.ctypes.data, Q.ctypes.data,
+                                                 H.ctypes.data) == 0
+            np.testing.assert_array_equal(A, O.setup_mapping_matrix(N, T))
+            np.testing.assert_allclose(Q, O.quadratic_cost_jacobian(N, r, T), rtol=1e-15, atol=0)
+            Ai_ref = O.invert_mapping_matrix(A)
+            # (the FP64 Schur inverse of the reference path loses up to ~2e-11 at N = 12, T = 0.013)
+            assert np.max(np.abs(Ai - Ai_ref) / np.maximum(np.abs(Ai_ref), 1e-300)) < 1e-9
+            H_ref = Ai_ref.T @ Q @ Ai_ref
+            scale = np.sqrt(np.outer(np.abs(np.diag(H_ref)), np.abs(np.diag(H_ref)))) + 1e-300
+            # forming A^-T Q A^-1 in FP64 (the reference path) costs digits at N = 12: 1.1e-7 at
+            # T = 0.013; the exact table is the accurate side
+            assert np.max(np.abs(H - H_ref) / scale) < (1e-8 if N <= 10 else 1e-6)
+    assert lib.mtg_host_segment_matrices(10, 4, 0.0, None, None, None, None) == nat.MTG_ERR_INVALID_ARGUMENT
+    assert lib.mtg_host_segment_matrices(10, 5, 1.0, None, None, None, None) == nat.MTG_ERR_BAD_DERIVATIVE
+    del ctypes

@@ -4,7 +4,7 @@ Pins, in order of strength:
   * the reference's known-answer test 2_vertices_setup (test/test_polynomial_optimization.cpp:700-744)
   * its A-matrix inversion test (:194-204), here against the exact rational inverse
   * the C++ standard's std::mt19937 known answer, and bit-equality of the restated
-    generators with the real libstdc++ ones (compiled into libmtg.so's host utilities)
+    generators with the real libstdc++ ones (compiled into libmav_trajectory_generation.so's host utilities)
   * 60-digit mpmath truth fixtures (tests/golden/, make_golden.py)
   * the reference's invariant tests: checkPath (:73-131), checkCost (:133-152),
     ConstraintPacking (:777-836), vertex generation (:154-192), 2_vertices_rand (:747-774)
