@@ -74,7 +74,7 @@ __device__ __forceinline__ double ldlt(double (&S)[H][H], double (&dinv)[H]) {
       w[k] = S[j][k] * dg[k];
       dj -= S[j][k] * w[k];
     }
-    pmin = dj < pmin ? dj : pmin;
+    pmin = (dj < pmin || dj != dj) ? dj : pmin;  // a NaN pivot sticks (NOT_SPD)
     const double inv = rcp(dj);
     dg[j] = dj;
     dinv[j] = inv;

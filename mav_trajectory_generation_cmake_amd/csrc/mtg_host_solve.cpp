@@ -63,7 +63,7 @@ struct HostSolve {
         w[k] = S[j][k] * dg[k];
         dj -= S[j][k] * w[k];
       }
-      pmin = dj < pmin ? dj : pmin;
+      pmin = (dj < pmin || dj != dj) ? dj : pmin;  // a NaN pivot sticks (NOT_SPD)
       const double inv = 1.0 / dj;
       dg[j] = dj;
       dinv[j] = inv;
@@ -247,7 +247,7 @@ struct HostSolve {
       }
       double dinv[H];
       const double pv = ldlt(S, dinv);
-      pmin = pv < pmin ? pv : pmin;
+      pmin = (pv < pmin || pv != pv) ? pv : pmin;  // a NaN pivot sticks (NOT_SPD)
       if (v < K) {  // G_v columns: E_v (top-right block of H_v) pinned
         const double* s = PW + (size_t)v * H;
         const double f = SCl[v];

@@ -186,7 +186,7 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
     __syncthreads();
     double dinv[H], x[H];
     const double pv = ldlt<H>(S, dinv);
-    pmin = pv < pmin ? pv : pmin;
+    pmin = (pv < pmin || pv != pv) ? pv : pmin;  // a NaN pivot sticks (NOT_SPD)
     ldlt_solve<H>(S, dinv, rhs, x);
     if (is_g && has_next) {
 #pragma unroll

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(128) void block_cholesky_kernel(SolveArgs a, double
     }
     double dinv[H];
     const double pv = ldlt<H>(S, dinv);
-    pmin = pv < pmin ? pv : pmin;
+    pmin = (pv < pmin || pv != pv) ? pv : pmin;  // a NaN pivot sticks (NOT_SPD)
     for (int d = 0; d < D; ++d) {  // z_v
       double r[H], z[H];
 #pragma unroll

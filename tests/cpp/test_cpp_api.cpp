@@ -173,7 +173,9 @@ static void test_random_paths(int D, int K, int max_derivative, int r, int seeds
           const VectorXd c = segments[i][d].getCoefficients();
           for (int j = 0; j < N; ++j) EXPECT(c[j] == coeffs[((size_t)i * D + d) * N + j], "batch vs single");
         }
-      EXPECT(std::fabs(bcost[0] - cost) <= 1e-9 * std::fmax(cost, 1e-12), "batch cost %g vs %g", bcost[0], cost);
+      // (computeCost forms Q with pow() the reference's way, lin_impl:574-589; the kernel's cost uses
+      // the exact table: at N = 12 the two differ in the 8th digit)
+      EXPECT(std::fabs(bcost[0] - cost) <= 1e-7 * std::fmax(cost, 1e-12), "batch cost %.17g vs %.17g", bcost[0], cost);
     }
   }
 }
