@@ -4,11 +4,13 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mtg.h"
@@ -29,6 +31,16 @@ struct mtg_ctx {
   int64_t launches = 0;
   std::string last_error;
   std::mutex mu;
+  // Pipelined host-pointer solves (run_solve_pipelined): kPipeSlots chunks in flight, each with its
+  // own stream (H2D -> kernel -> D2H) and device buffers.
+  static constexpr int kPipeSlots = 4;
+  struct PipeSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    void* dev = nullptr;  // device inputs + outputs of one chunk
+    size_t dev_bytes = 0;
+  } pipe[kPipeSlots];
+  hipEvent_t pipe_start = nullptr;
 };
 
 namespace mtg {
@@ -149,6 +161,164 @@ int check_shape(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch) {
   return MTG_OK;
 }
 
+hipError_t ensure_pipe(mtg_ctx* ctx) {
+  if (ctx->pipe_start) return hipSuccess;
+  for (auto& s : ctx->pipe) {
+    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  return hipEventCreateWithFlags(&ctx->pipe_start, hipEventDisableTiming);
+}
+
+void destroy_pipe(mtg_ctx* ctx) {
+  for (auto& s : ctx->pipe) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.dev) (void)hipFree(s.dev);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = mtg_ctx::PipeSlot{};
+  }
+  if (ctx->pipe_start) (void)hipEventDestroy(ctx->pipe_start);
+  ctx->pipe_start = nullptr;
+}
+
+// host-pointer solves above this size go through the chunked pipeline
+constexpr size_t kPipelineMinBytes = 8u << 20;
+
+// Host-pointer batch solve as a pipeline of chunks (the reference's equivalent is a
+// loop of single solves, src/polynomial_timing_evaluation.cpp:119-126).  Each of kPipeSlots slots
+// has its own stream and device buffers.  This thread issues, per chunk, the H2D copies and the
+// kernel; a second host thread issues the chunk's D2H copies and retires it.  So the H2D of chunk
+// c+1 runs on one DMA direction while the D2H of chunk c runs on the other (PCIe is full duplex:
+// ~57 GB/s each way on MI355X, 97 GB/s both, scripts/pcie_bw.py), whether the caller's arrays are
+// pinned (asynchronous copies) or pageable (the runtime's own staging, which blocks the issuing
+// thread -- hence two threads).  A slot is reused only after its previous chunk's D2H completed.
+int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const double* values,
+                        const uint8_t* mask, const double* times, double* coeffs, double* free_out,
+                        int32_t* n_free_out, double* cost_out, int32_t* status, bool general) {
+  constexpr int S = mtg_ctx::kPipeSlots;
+  const int V = K + 1, h = N / 2;
+  // per-trajectory bytes of each array
+  const size_t s_vals = sizeof(double) * (size_t)V * h * D, s_mask = (size_t)V, s_times = sizeof(double) * K;
+  const size_t s_coef = coeffs ? sizeof(double) * (size_t)K * D * N : 0;
+  const size_t s_free = free_out ? sizeof(double) * D * V * h : 0;
+  const size_t s_nfree = n_free_out ? sizeof(int32_t) : 0, s_cost = cost_out ? sizeof(double) : 0;
+  const size_t s_status = status ? sizeof(int32_t) : 0;
+  const size_t per_traj = s_vals + s_mask + s_times + s_coef + s_free + s_nfree + s_cost + s_status;
+  // a quarter of the batch per chunk (the pipeline fills and drains in a quarter of the run), at
+  // most ~32 MB of traffic per chunk (per-chunk issue costs stay below ~5%)
+  int64_t chunk = std::min<int64_t>((batch + 3) / 4, (int64_t)((32u << 20) / per_traj));
+  chunk = (std::max<int64_t>(chunk, 1024) + 63) / 64 * 64;
+  const int64_t n_chunks = (batch + chunk - 1) / chunk;
+  size_t off = 0;  // one slot's device layout, 256-B aligned sub-buffers
+  const size_t o_vals = off; off = align_up(off + s_vals * chunk);
+  const size_t o_mask = off; off = align_up(off + s_mask * chunk);
+  const size_t o_times = off; off = align_up(off + s_times * chunk);
+  const size_t o_coef = off; off = align_up(off + s_coef * chunk);
+  const size_t o_free = off; off = align_up(off + s_free * chunk);
+  const size_t o_nfree = off; off = align_up(off + s_nfree * chunk);
+  const size_t o_cost = off; off = align_up(off + s_cost * chunk);
+  const size_t o_status = off; off = align_up(off + s_status * chunk);
+  MTG_HIP_TRY(ctx, ensure_pipe(ctx));
+  for (auto& s : ctx->pipe) MTG_HIP_TRY(ctx, ensure(&s.dev, &s.dev_bytes, off));
+  // order after whatever the caller queued on the context's stream
+  MTG_HIP_TRY(ctx, hipEventRecord(ctx->pipe_start, ctx->stream));
+  for (auto& s : ctx->pipe) MTG_HIP_TRY(ctx, hipStreamWaitEvent(s.stream, ctx->pipe_start, 0));
+
+  std::mutex m;
+  std::condition_variable cv;
+  int64_t launched = 0, retired = 0;  // chunks whose kernel is queued / whose outputs have landed
+  hipError_t err = hipSuccess;
+  const char* err_what = "";
+  auto fail = [&](hipError_t e, const char* what) {
+    std::lock_guard<std::mutex> g(m);
+    if (err == hipSuccess) err = e, err_what = what;
+    cv.notify_all();
+  };
+  // D2H issuer: chunk c's outputs into the caller's arrays, on the chunk's slot stream (ordered after
+  // its kernel), then wait for them and retire the chunk
+  std::thread d2h([&] {
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return fail(e, "hipSetDevice");
+    for (int64_t c = 0; c < n_chunks; ++c) {
+      {
+        std::unique_lock<std::mutex> l(m);
+        cv.wait(l, [&] { return launched > c || err != hipSuccess; });
+        if (err != hipSuccess) return;
+      }
+      mtg_ctx::PipeSlot& s = ctx->pipe[c % S];
+      const int64_t b0 = c * chunk, nb = std::min<int64_t>(chunk, batch - b0);
+      const char* dp = static_cast<const char*>(s.dev);
+      auto copy = [&](void* user, size_t o, size_t sz) -> hipError_t {
+        return sz ? hipMemcpyAsync((char*)user + b0 * sz, dp + o, nb * sz, hipMemcpyDeviceToHost, s.stream)
+                  : hipSuccess;
+      };
+      e = copy(coeffs, o_coef, s_coef);
+      if (e == hipSuccess) e = copy(free_out, o_free, s_free);
+      if (e == hipSuccess) e = copy(n_free_out, o_nfree, s_nfree);
+      if (e == hipSuccess) e = copy(cost_out, o_cost, s_cost);
+      if (e == hipSuccess) e = copy(status, o_status, s_status);
+      if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+      // retire the previous chunk (its copies queued before this one's, so the DMA engine never
+      // idles between chunks while this thread waits), and the last one at the end
+      if (e == hipSuccess && c > 0) e = hipEventSynchronize(ctx->pipe[(c - 1) % S].done);
+      if (e == hipSuccess && c + 1 == n_chunks) e = hipEventSynchronize(s.done);
+      if (e != hipSuccess) return fail(e, "pipelined D2H");
+      std::lock_guard<std::mutex> g(m);
+      retired = c + 1 == n_chunks ? n_chunks : c;
+      cv.notify_all();
+    }
+  });
+  // H2D + kernel issuer (this thread)
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    {
+      std::unique_lock<std::mutex> l(m);  // the slot's previous chunk must have landed
+      cv.wait(l, [&] { return retired >= c - S + 1 || err != hipSuccess; });
+      if (err != hipSuccess) break;
+    }
+    mtg_ctx::PipeSlot& s = ctx->pipe[c % S];
+    const int64_t b0 = c * chunk, nb = std::min<int64_t>(chunk, batch - b0);
+    char* dp = static_cast<char*>(s.dev);
+    hipError_t e = hipMemcpyAsync(dp + o_vals, (const char*)values + b0 * s_vals, nb * s_vals,
+                                  hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(dp + o_mask, (const char*)mask + b0 * s_mask, nb * s_mask, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(dp + o_times, (const char*)times + b0 * s_times, nb * s_times, hipMemcpyHostToDevice,
+                         s.stream);
+    if (e == hipSuccess && free_out) e = hipMemsetAsync(dp + o_free, 0, nb * s_free, s.stream);
+    if (e == hipSuccess) {
+      mtg::SolveArgs a{};
+      a.B = nb;
+      a.K = K;
+      a.D = D;
+      a.r = r;
+      a.n_cand = 1;
+      a.values = reinterpret_cast<const double*>(dp + o_vals);
+      a.mask = reinterpret_cast<const uint8_t*>(dp + o_mask);
+      a.times = reinterpret_cast<const double*>(dp + o_times);
+      a.coeffs = coeffs ? reinterpret_cast<double*>(dp + o_coef) : nullptr;
+      a.free_out = free_out ? reinterpret_cast<double*>(dp + o_free) : nullptr;
+      a.n_free_out = n_free_out ? reinterpret_cast<int32_t*>(dp + o_nfree) : nullptr;
+      a.cost_out = cost_out ? reinterpret_cast<double*>(dp + o_cost) : nullptr;
+      a.status = status ? reinterpret_cast<int32_t*>(dp + o_status) : nullptr;
+      e = mtg::launch_solve(N, a, s.stream, general);
+    }
+    if (e != hipSuccess) {
+      fail(e, "pipelined H2D / launch");
+      break;
+    }
+    std::lock_guard<std::mutex> g(m);
+    launched = c + 1;
+    cv.notify_all();
+  }
+  d2h.join();
+  for (auto& s : ctx->pipe) (void)hipStreamSynchronize(s.stream);  // nothing may still read the caller's arrays
+  if (err != hipSuccess) return set_hip_error(ctx, err, err_what);
+  return MTG_OK;
+}
+
 // Shared body of solve / time-sweep: stage host buffers if needed, launch, copy back.
 int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const double* values,
               const uint8_t* mask, const double* times, double* coeffs, double* free_out,
@@ -157,6 +327,10 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   const int V = K + 1, h = N / 2;
   const int64_t pairs = batch * n_cand;
   MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 &&
+      (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes)
+    return run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out, cost_out,
+                               status, (flags & MTG_FLAG_GENERAL_KERNEL) != 0);
   mtg::SolveArgs a{};
   a.B = pairs;
   a.K = K;
@@ -345,6 +519,7 @@ int mtg_destroy(mtg_ctx* ctx) {
   if (ctx->staging) (void)hipFree(ctx->staging);
   if (ctx->workspace) (void)hipFree(ctx->workspace);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  destroy_pipe(ctx);
   destroy_events(ctx);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;

@@ -564,3 +564,86 @@ def test_not_spd_status(gpu_ctx, path):
             assert out["status"][b] & nat.MTG_TRAJ_NOT_SPD, (b, out["status"][b])
         else:
             assert out["status"][b] == 0, (b, out["status"][b])
+
+
+def test_config3_one_million_as_eight_shards(gpu_ctx):
+    """BASELINE config 3: 1e6 config-2 trajectories (seeds 0 .. 1e6-1) as the 8 contiguous shards of
+    125000 that bench.py gives 8 ranks.  The shards, solved separately, concatenate bit-equal to one
+    launch over the whole batch; every trajectory passes the relative checkPath; a 2000-trajectory
+    sample matches the oracle (disagreements above 1e-6 arbitrated by 60-digit truth)."""
+    torch = pytest.importorskip("torch")
+    import os
+    import sys
+    O = _oracle()
+    B, G = 1_000_000, 8
+    vals, mask, times = _bench_batch(B, seed0=0)
+    v_d, m_d, t_d = (torch.from_numpy(x).cuda() for x in (vals, mask, times))
+    whole = gpu_ctx.solve_linear_batch(10, 4, v_d, m_d, t_d, status=True)["coeffs"]
+    shard = B // G
+    parts = [gpu_ctx.solve_linear_batch(10, 4, v_d[g * shard:(g + 1) * shard], m_d[g * shard:(g + 1) * shard],
+                                        t_d[g * shard:(g + 1) * shard], status=True) for g in range(G)]
+    torch.cuda.synchronize()
+    for g, p in enumerate(parts):
+        assert bool(torch.equal(p["coeffs"], whole[g * shard:(g + 1) * shard])), g
+        assert int(p["status"].abs().sum()) == 0, g
+    coeffs = whole.cpu().numpy()
+    del whole, parts
+    assert np.all(np.isfinite(coeffs))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import truth_solve
+    # relative checkPath on every trajectory, in blocks of 1000.  Where it exceeds 1e-6, the check
+    # itself is at its FP64 limit (p^(k) of a sub-millisecond segment cancels among c_j T^j, DESIGN.md
+    # "Parity"): such a trajectory passes if its coefficients are within TRUTH_TOL of 60-digit truth
+    # (scale-normalised) or if the check is within twice what truth's own rounded coefficients give.
+    # (Seed 107250 has a 0.14 ms segment: this kernel is 1.0e-13 from truth with checkPath 1.2e-6;
+    # the reference algorithm is 6.8e-10 from truth with checkPath 3.0e-4.)
+    outliers = []
+    for b0 in range(0, B, 1000):
+        sl = slice(b0, b0 + 1000)
+        if check_path(vals[sl], mask[sl], times[sl], coeffs[sl], 10, relative=True) >= 1e-6:
+            outliers += [b for b in range(b0, b0 + 1000)
+                         if check_path(vals[b:b + 1], mask[b:b + 1], times[b:b + 1], coeffs[b:b + 1], 10,
+                                       relative=True) >= 1e-6]
+    assert len(outliers) <= 20, len(outliers)
+    for b in outliers:
+        tr = truth_solve(10, 4, vals[b], mask[b], times[b])[0]
+        e_gpu = check_path(vals[b:b + 1], mask[b:b + 1], times[b:b + 1], coeffs[b:b + 1], 10, relative=True)
+        e_tr = check_path(vals[b:b + 1], mask[b:b + 1], times[b:b + 1], tr[None], 10, relative=True)
+        e_coef = scale_normalised_error(coeffs[b:b + 1], tr[None], times[b:b + 1])
+        assert e_coef <= TRUTH_TOL or e_gpu <= max(1e-6, 2 * e_tr), (b, e_gpu, e_tr, e_coef)
+    rng = np.random.default_rng(3)
+    idx = np.sort(rng.choice(B, 2000, replace=False))
+    ref = O.solve_linear_batch(10, 4, vals[idx], mask[idx].astype(np.uint32), times[idx])
+    errs = np.array([scale_normalised_error(coeffs[i:i + 1], ref[j:j + 1], times[i:i + 1]) for j, i in enumerate(idx)])
+    bad = np.nonzero(errs > ORACLE_TOL_N10)[0]
+    assert len(bad) <= 5, np.sort(errs)[-10:]
+    for j in bad:
+        i = int(idx[j])
+        tr = truth_solve(10, 4, vals[i], mask[i], times[i])[0]
+        e_gpu = scale_normalised_error(coeffs[i:i + 1], tr[None], times[i:i + 1])
+        e_ref = scale_normalised_error(ref[j:j + 1], tr[None], times[i:i + 1])
+        assert e_gpu <= max(ORACLE_TOL_N10, e_ref), (i, e_gpu, e_ref)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_pipelined_host_arrays(gpu_ctx, pinned):
+    """Host-array batches above 8 MB run as a pipeline of chunks on 3 streams (H2D, kernel and D2H
+    of different chunks overlapping): bit-equal to the device-pointer launch, from pageable memory
+    (staged through pinned buffers) and from pinned memory (DMA'd in place), with a ragged tail."""
+    torch = pytest.importorskip("torch")
+    B = 50_001
+    vals, mask, times = _bench_batch(B, seed0=777)
+    dev = gpu_ctx.solve_linear_batch(10, 4, torch.from_numpy(vals).cuda(), torch.from_numpy(mask).cuda(),
+                                     torch.from_numpy(times).cuda(), free=True, n_free=True, cost=True, status=True)
+    torch.cuda.synchronize()
+    if pinned:
+        tv, tm, tt = (torch.from_numpy(x).pin_memory() for x in (vals, mask, times))
+        out = {k: torch.empty(tuple(v.shape), dtype=v.dtype).pin_memory() for k, v in dev.items()}
+        gpu_ctx.solve_linear_batch(10, 4, tv.numpy(), tm.numpy(), tt.numpy(), coeffs=out["coeffs"].numpy(),
+                                   free=out["free"].numpy(), n_free=out["n_free"].numpy(), cost=out["cost"].numpy(),
+                                   status=out["status"].numpy())
+        host = {k: v.numpy() for k, v in out.items()}
+    else:
+        host = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, free=True, n_free=True, cost=True, status=True)
+    for k in ("coeffs", "free", "n_free", "cost", "status"):
+        np.testing.assert_array_equal(host[k], dev[k].cpu().numpy(), err_msg=k)
