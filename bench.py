@@ -215,6 +215,8 @@ def main():
     ap.add_argument("--split", action="store_true", help="two-kernel path (assembly + block Cholesky)")
     ap.add_argument("--general-kernel", action="store_true",
                     help="force the general LDS-resident fused kernel (A/B against the default)")
+    ap.add_argument("--lane-kernel", action="store_true",
+                    help="the lane-per-chain kernel where it applies (A/B against the default)")
     args = ap.parse_args()
 
     import torch
@@ -263,14 +265,13 @@ def main():
     else:
         out_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
         # one step = one launch of the solve on torch's current stream
-        step = ctx.solve_call(N, r, v_d, m_d, t_d, out_d, split=args.split, general=args.general_kernel)
-        step_t = ctx_t.solve_call(N, r, v_d, m_d, t_d, out_d, split=args.split, general=args.general_kernel)
-        if args.split:
-            kname = "assemble+block_cholesky"
-        elif args.general_kernel or K > 20 or (K > 12 and N != 12) or (N == 12 and 8 < K <= 12):
-            kname = "solve_fused_kernel"
-        else:
-            kname = "solve_reg_kernel"
+        kw = dict(split=args.split, general=args.general_kernel, lane=args.lane_kernel)
+        step = ctx.solve_call(N, r, v_d, m_d, t_d, out_d, **kw)
+        step_t = ctx_t.solve_call(N, r, v_d, m_d, t_d, out_d, **kw)
+        nat = mtg._native
+        kflags = ((nat.MTG_FLAG_SPLIT_KERNELS if args.split else 0) | (nat.MTG_FLAG_GENERAL_KERNEL if args.general_kernel else 0)
+                  | (nat.MTG_FLAG_LANE_KERNEL if args.lane_kernel else 0))
+        kname = mtg._native.solve_kernel(N, D, K, r, kflags)
     stride = max(1, args.timing_stride)
     timed_steps = [i for i in range(args.steps) if i % stride == 0]
     ctx.enable_timing(0)

@@ -71,13 +71,27 @@ extern "C" {
 #define MTG_FLAG_ASYNC 2u              /* do not synchronize the stream before returning */
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
 #define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
-                                          (default: the register-resident kernel when K <= 12, and
-                                          for N = 12 when K <= 20) */
+                                          (default: see mtg_solve_kernel) */
+#define MTG_FLAG_LANE_KERNEL 16u       /* the lane-per-chain kernel where it applies (N in {6, 8, 10},
+                                          D <= 4, K <= 10; a fifth of the default kernel's
+                                          instructions per trajectory, but latency-bound at one wave
+                                          per SIMD: DESIGN.md 3.2) */
+
+/* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
+#define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave
+                                          (MTG_FLAG_LANE_KERNEL) */
+#define MTG_KERNEL_COLUMN 2            /* default: register column kernel, a lane per column of G_v /
+                                          per dimension, twisted (K <= 12, N = 12 up to K = 20) */
+#define MTG_KERNEL_GENERAL 3           /* general LDS-resident fused kernel (any K) */
+#define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
 
 typedef struct mtg_ctx mtg_ctx;
 
 /* Version / diagnostics. */
 int mtg_abi_version(void);
+/* The solve kernel (MTG_KERNEL_*) mtg_solve_linear_batch runs for this shape and these flags, or a
+   negative MTG_ERR_* for a shape it rejects.  No device work. */
+int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned flags);
 const char* mtg_status_string(int code);
 const char* mtg_last_error(mtg_ctx* ctx);
 

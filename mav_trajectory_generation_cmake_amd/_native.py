@@ -31,11 +31,20 @@ MTG_FLAG_DEVICE_PTRS = 1
 MTG_FLAG_ASYNC = 2
 MTG_FLAG_SPLIT_KERNELS = 4
 MTG_FLAG_GENERAL_KERNEL = 8
+MTG_FLAG_LANE_KERNEL = 16
+
+MTG_KERNEL_LANE = 1
+MTG_KERNEL_COLUMN = 2
+MTG_KERNEL_GENERAL = 3
+MTG_KERNEL_SPLIT = 4
+KERNEL_NAMES = {MTG_KERNEL_LANE: "solve_lane_kernel", MTG_KERNEL_COLUMN: "solve_reg_kernel",
+                MTG_KERNEL_GENERAL: "solve_fused_kernel", MTG_KERNEL_SPLIT: "assemble+block_cholesky"}
 
 _c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
 
 _SIGNATURES = {
     "mtg_abi_version": (ctypes.c_int, []),
+    "mtg_solve_kernel": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
     "mtg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "mtg_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "mtg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
@@ -165,6 +174,14 @@ def check(code, ctx=None):
                 msg += ": " + detail.decode()
         raise MTGError(code, msg)
     return code
+
+
+def solve_kernel(N, D, K, r, flags=0):
+    """Name of the solve kernel mtg_solve_linear_batch runs for this shape (mtg_solve_kernel)."""
+    code = load().mtg_solve_kernel(N, D, K, r, flags)
+    if code < 0:
+        raise MTGError(code, status_string(code))
+    return KERNEL_NAMES[code]
 
 
 def device_count():

@@ -196,7 +196,7 @@ constexpr size_t kPipelineMinBytes = 8u << 20;
 // thread -- hence two threads).  A slot is reused only after its previous chunk's D2H completed.
 int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const double* values,
                         const uint8_t* mask, const double* times, double* coeffs, double* free_out,
-                        int32_t* n_free_out, double* cost_out, int32_t* status, bool general) {
+                        int32_t* n_free_out, double* cost_out, int32_t* status, unsigned kflags) {
   constexpr int S = mtg_ctx::kPipeSlots;
   const int V = K + 1, h = N / 2;
   // per-trajectory bytes of each array
@@ -303,7 +303,7 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       a.n_free_out = n_free_out ? reinterpret_cast<int32_t*>(dp + o_nfree) : nullptr;
       a.cost_out = cost_out ? reinterpret_cast<double*>(dp + o_cost) : nullptr;
       a.status = status ? reinterpret_cast<int32_t*>(dp + o_status) : nullptr;
-      e = mtg::launch_solve(N, a, s.stream, general);
+      e = mtg::launch_solve(N, a, s.stream, kflags);
     }
     if (e != hipSuccess) {
       fail(e, "pipelined H2D / launch");
@@ -330,7 +330,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 &&
       (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes)
     return run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out, cost_out,
-                               status, (flags & MTG_FLAG_GENERAL_KERNEL) != 0);
+                               status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL));
   mtg::SolveArgs a{};
   a.B = pairs;
   a.K = K;
@@ -429,7 +429,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, (flags & MTG_FLAG_GENERAL_KERNEL) != 0));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL)));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (pin) {
@@ -461,6 +461,17 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
 extern "C" {
 
 int mtg_abi_version(void) { return MTG_ABI_VERSION; }
+
+int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned flags) {
+  if (N < 2 || N > 12 || (N % 2)) return MTG_ERR_UNSUPPORTED_N;
+  if (derivative_to_optimize < 0 || derivative_to_optimize > N / 2 - 1) return MTG_ERR_BAD_DERIVATIVE;
+  if (K < 1 || D < 1) return MTG_ERR_SIZE_MISMATCH;
+  int lg, tpb;
+  size_t lds;
+  if (!mtg::solve_geometry(N, D, K, &lg, &lds, &tpb)) return MTG_ERR_TOO_LARGE;
+  if (flags & MTG_FLAG_SPLIT_KERNELS) return MTG_KERNEL_SPLIT;
+  return mtg::solve_kernel(N, D, K, flags);
+}
 
 const char* mtg_status_string(int code) {
   switch (code) {

@@ -22,6 +22,12 @@ constexpr int kBlock = 64;
 constexpr size_t kMaxLdsPerBlock = 64 * 1024;
 constexpr size_t kMaxLdsHard = 160 * 1024;
 
+// Orders this wave's LDS accesses (every block is one wave): waits for its LDS operations only,
+// and is a compiler memory barrier.  __syncthreads() would also wait for the wave's outstanding
+// global stores (vmcnt counts stores on gfx9), which in a store-per-round epilogue exposes the
+// HBM write latency once per round.
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // 1/x from v_rcp_f64 plus two Newton steps (full FP64 accuracy; no IEEE division sequence).
 __device__ __forceinline__ double rcp(double x) {
   double y = __builtin_amdgcn_rcp(x);

@@ -51,13 +51,17 @@ struct SolveArgs {
 // when the per-trajectory working set cannot fit in LDS.
 bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes, int* traj_per_block);
 
-// Launch the fused solve on `stream`: the register-resident kernel (mtg_solve_reg.hip) when the
-// shape allows it (reg_geometry: K <= 12, or N = 12 with K <= 20; LDS slot fits) and `general` is
-// false, else the general LDS-resident
-// kernel (mtg_kernels.hip).
-hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, bool general = false);
+// Launch the fused solve on `stream` with the kernel solve_kernel() picks: the register column
+// kernel (mtg_solve_reg.hip) where reg_geometry allows it (K <= 12, or N = 12 with K <= 20), else
+// the general LDS-resident kernel (mtg_kernels.hip); MTG_FLAG_LANE_KERNEL selects the
+// lane-per-chain kernel (mtg_solve_lane.hip) where lane_geometry allows it, MTG_FLAG_GENERAL_KERNEL
+// the general kernel.
+int solve_kernel(int N, int D, int K, unsigned flags);  // MTG_KERNEL_LANE / _COLUMN / _GENERAL
+hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags = 0);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);
 hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
+bool lane_geometry(int N, int D, int K, size_t* lds_bytes);
+hipError_t launch_solve_lane(int N, const SolveArgs& a, hipStream_t stream);
 
 // Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
 // workspace, then the block-Cholesky solve + recovery.

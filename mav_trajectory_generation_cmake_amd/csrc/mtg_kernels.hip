@@ -407,10 +407,21 @@ static hipError_t launch_fused_n(const SolveArgs& a, hipStream_t stream) {
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, bool general) {
+int solve_kernel(int N, int D, int K, unsigned flags) {
   int lg;
   size_t lds;
-  if (!general && reg_geometry(N, a.D, a.K, &lg, &lds)) return launch_solve_reg(N, a, stream);
+  if (flags & MTG_FLAG_GENERAL_KERNEL) return MTG_KERNEL_GENERAL;
+  if ((flags & MTG_FLAG_LANE_KERNEL) && lane_geometry(N, D, K, &lds)) return MTG_KERNEL_LANE;
+  if (reg_geometry(N, D, K, &lg, &lds)) return MTG_KERNEL_COLUMN;
+  return MTG_KERNEL_GENERAL;
+}
+
+hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags) {
+  switch (solve_kernel(N, a.D, a.K, flags)) {
+    case MTG_KERNEL_LANE: return launch_solve_lane(N, a, stream);
+    case MTG_KERNEL_COLUMN: return launch_solve_reg(N, a, stream);
+    default: break;
+  }
   switch (N) {
     case 2: return launch_fused_n<2>(a, stream);
     case 4: return launch_fused_n<4>(a, stream);

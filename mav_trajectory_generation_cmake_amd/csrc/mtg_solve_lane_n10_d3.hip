@@ -1,0 +1,6 @@
+// One (N, D) of the lane-per-chain solve kernel (mtg_solve_lane.inc).
+#include "mtg_solve_lane.inc"
+
+namespace mtg {
+MTG_LANE_LAUNCHER(10, 3)
+}  // namespace mtg

@@ -87,7 +87,7 @@ class Context:
         return np.array(buf[:got.value], dtype=np.float64)
 
     def solve_call(self, N, r, values, mask, times, coeffs, free=None, n_free=None, cost=None, status=None,
-                   split=False, general=False):
+                   split=False, general=False, lane=False):
         """A zero-argument callable that launches one device-pointer solve asynchronously on the
         current stream with the arguments bound once (the bench's step; minimal host overhead)."""
         import torch
@@ -96,6 +96,7 @@ class Context:
         self.set_stream(torch.cuda.current_stream(values.device).cuda_stream)
         flags = nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC | (nat.MTG_FLAG_SPLIT_KERNELS if split else 0)
         flags |= nat.MTG_FLAG_GENERAL_KERNEL if general else 0
+        flags |= nat.MTG_FLAG_LANE_KERNEL if lane else 0
         fn = self._lib.mtg_solve_linear_batch
         args = (self.handle, N, D, K, r, B, _addr(values), _addr(mask), _addr(times), _addr(coeffs), _addr(free),
                 _addr(n_free), _addr(cost), _addr(status), flags)
@@ -145,7 +146,7 @@ class Context:
 
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
-                           cost=None, status=None, split=False, asynchronous=False, general=False):
+                           cost=None, status=None, split=False, asynchronous=False, general=False, lane=False):
         """Solve a batch; returns dict of outputs (allocates those not given).
 
         want-flags: pass arrays (or True to allocate) for free / n_free / cost / status."""
@@ -190,6 +191,8 @@ class Context:
             flags |= nat.MTG_FLAG_SPLIT_KERNELS
         if general:
             flags |= nat.MTG_FLAG_GENERAL_KERNEL
+        if lane:
+            flags |= nat.MTG_FLAG_LANE_KERNEL
         rc = self._lib.mtg_solve_linear_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                               _addr(times), _addr(coeffs), _addr(free), _addr(n_free),
                                               _addr(cost), _addr(status), flags)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-phase cycle counts of the register-resident kernel (debug build: make -C ... timing).
+"""Per-phase cycle counts of the register column kernel (debug build: cmake -DMTG_PHASE_TIMING=ON).
 
 Run: MTG_LIBRARY=mav_trajectory_generation_cmake_amd/lib_timing/libmav_trajectory_generation.so python scripts/phase_timing.py
 """

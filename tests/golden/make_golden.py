@@ -15,6 +15,7 @@ Run from the repo root:  python tests/golden/make_golden.py
 import os
 import sys
 import time
+from concurrent.futures import ProcessPoolExecutor
 
 import mpmath as mp
 import numpy as np
@@ -110,8 +111,9 @@ def write_case(name, N, r, problems, note):
     B, V, nd, D = vals.shape
     K = V - 1
     coeffs, costs, frees, fixeds = [], [], [], []
-    for b in range(B):
-        c, cost, fr, fx = truth_solve(N, r, vals[b], mask[b], times[b])
+    with ProcessPoolExecutor(max_workers=min(B, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(truth_solve, [N] * B, [r] * B, list(vals), list(mask), list(times)))
+    for c, cost, fr, fx in res:
         coeffs.append(c)
         costs.append(cost)
         frees.append(fr)
@@ -179,7 +181,14 @@ def mixed(seed, N, K, D, B):
     return out
 
 
-def main():
+def main(only=None):
+    if only is not None:  # regenerate one case: python tests/golden/make_golden.py <name>
+        global write_case
+        _write = write_case
+
+        def write_case(name, *a):
+            if name == only:
+                _write(name, *a)
     # 2_vertices_setup known answer (test/test_polynomial_optimization.cpp:700-744)
     v = np.zeros((2, 5, 1))
     v[1, 0, 0] = 5.0
@@ -189,7 +198,7 @@ def main():
                "createRandomVertices(SNAP,3,[-10,-20,-10],[10,20,10],seed) + estimateSegmentTimes(3,5)")
     write_case("cfg2_n10_k10", 10, 4, cfg2(list(range(12))),
                "createRandomVerticesPath(3,10,5.0,SNAP,seed) + estimateSegmentTimes(2,2,6.5)")
-    write_case("cfg4_n12_k20_jerk", 12, 3, cfg4(list(range(5))),
+    write_case("cfg4_n12_k20_jerk", 12, 3, cfg4(list(range(32))),
                "createRandomVertices(SNAP,20,[-10,-20,-10],[10,20,10],seed), r=JERK, times estimateSegmentTimes(3,5)")
     # ConstraintPacking shape: K=5, ends to JERK, D=3, N=10 default r=4
     cp = []
@@ -211,4 +220,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -17,9 +17,11 @@ pytestmark = pytest.mark.gpu
 TRUTH_TOL = 1e-9
 ORACLE_TOL_N10 = 1e-6
 
-# the three solve paths behind mtg_solve_linear_batch: the default (register-resident kernel for
-# K <= 12 and for N = 12 up to K = 20, else the general one), the general LDS-resident fused kernel, and the two-kernel split path
-PATHS = {"default": {}, "general": {"general": True}, "split": {"split": True}}
+# the solve paths behind mtg_solve_linear_batch: the default (mtg_solve_kernel: the register column
+# kernel for K <= 12 and for N = 12 up to K = 20, else the general one), the lane-per-chain kernel
+# (MTG_FLAG_LANE_KERNEL, where it applies), the general LDS-resident fused kernel, and the two-kernel
+# split path
+PATHS = {"default": {}, "lane": {"lane": True}, "general": {"general": True}, "split": {"split": True}}
 
 
 def _oracle():
@@ -211,7 +213,7 @@ def test_paths_agree_mixed_masks(gpu_ctx):
     for p, o in outs.items():
         assert np.all(o["status"] == 0), p
         assert scale_normalised_error(o["coeffs"], ref, times) <= 1e-6, p
-    for p in ("general", "split"):
+    for p in ("lane", "general", "split"):
         assert scale_normalised_error(outs[p]["coeffs"], outs["default"]["coeffs"], times) <= 1e-9, p
 
 

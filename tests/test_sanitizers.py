@@ -1,0 +1,34 @@
+"""ASan/UBSan on the host code: the library's host sources (csrc/mtg_host.cpp,
+csrc/mtg_host_solve.cpp) and the oracle restatement (oracle/mtg_oracle.c), compiled with
+-fsanitize=address,undefined and driven by tests/sanitize/sanitize_driver.cpp.  Host code only: GPU
+sanitizers are not available on this pool.  The oracle is test infrastructure; it is compiled here
+as the checker the driver compares against."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mav_trajectory_generation_cmake_amd", "csrc")
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="needs gcc/g++")
+def test_host_code_under_asan_ubsan(tmp_path):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)  # the sanitizer runtime must come first in the process
+    oracle_o = tmp_path / "oracle.o"
+    subprocess.check_call(["gcc", "-std=c99", "-c", "-o", str(oracle_o), os.path.join(ROOT, "oracle", "mtg_oracle.c"),
+                           "-I", os.path.join(ROOT, "oracle")] + SAN)
+    exe = tmp_path / "sanitize_driver"
+    subprocess.check_call(["g++", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                           os.path.join(ROOT, "tests", "sanitize", "sanitize_driver.cpp"),
+                           os.path.join(CSRC, "mtg_host.cpp"), os.path.join(CSRC, "mtg_host_solve.cpp"), str(oracle_o),
+                           "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-I", os.path.join(ROOT, "oracle"),
+                           "-lpthread", "-lm"] + SAN)
+    r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert "0 failed checks" in r.stdout
