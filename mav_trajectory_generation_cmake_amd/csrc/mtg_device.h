@@ -64,6 +64,14 @@ __device__ __forceinline__ void load_fixed(const double* vals, int v, int D, int
   }
 }
 
+// Running minimum of the LDL^T pivots in which a NaN pivot sticks (NOT_SPD is reported for a
+// minimum <= 0 or not finite): v_min_f64 returns the other operand for a quiet NaN, so a NaN pivot
+// is folded in as -inf.  Two VALU operations (compare-unordered + select folds into the min's
+// operand) instead of a compare/compare/or/select pair.
+__device__ __forceinline__ double pivot_min(double pmin, double dj) {
+  return __builtin_fmin(pmin, dj != dj ? -__builtin_inf() : dj);
+}
+
 // S = L diag(d) L^T (L unit lower, below the diagonal of S; only the lower triangle of S is
 // read); dinv = 1/d.  Returns the smallest pivot (<= 0 or non-finite: R_pp is not SPD; the
 // reference never checks, lin_impl:355-368).
