@@ -15,14 +15,11 @@ hipError_t launch_solve_reg_n12(const SolveArgs&, int, size_t, hipStream_t);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes) {
   const int H = N / 2;
   // G_v columns take H * KMAX doubles per lane: beyond ~50 the 2-waves-per-SIMD kernel spills
-  // (N=12, K > 8); the wide bucket (N = 12, K <= 20) splits G over two lane sets instead
+  // (N=12, K > 8); the wide bucket (N = 12, K <= 20) keeps G in LDS instead (Forward::GLDS)
   const int km = reg_kmax(K);
   if (km < 0 || (H * km > 50 && !(N == 12 && km == kRegKMaxWide))) return false;
   int lc = 8;  // lanes per chain: h column lanes + D dimension lanes
   while (lc < H + D) lc *= 2;
-  // the wide bucket parks half of a chain's G_v on lanes 9..14 of the chain's lanes: it needs 16
-  // lanes per chain even when H + D <= 8 (N = 12 with D = 1 or 2)
-  if (N == 12 && km == kRegKMaxWide && lc < kRegWideMinLanes) lc = kRegWideMinLanes;
   const int lg = kTwist ? 2 * lc : lc;  // twisted: two chains per trajectory
   if (lg > 64) return false;
   const size_t bytes = (size_t)reg_lds_doubles(N, D, K, lg, kTwist) * sizeof(double);
