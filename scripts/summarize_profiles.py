@@ -35,8 +35,17 @@ def counter_means(path, skip_first=2):
     of each kernel (warm-up)."""
     per = {}
     seen = {}
-    for r in _rows(path):
+    rows = _rows(path)
+    # only the bench's own launches: per kernel, the dispatches with the largest grid (the
+    # end_to_end leg's pipeline chunks launch the same kernel on smaller grids)
+    grid = {}
+    for r in rows:
+        grid[r["Kernel_Name"]] = max(grid.get(r["Kernel_Name"], 0), int(r.get("Grid_Size", 0) or 0))
+    rows = [r for r in rows if int(r.get("Grid_Size", 0) or 0) == grid[r["Kernel_Name"]]]
+    for r in rows:
         k = r["Kernel_Name"]
+        if k.startswith("__amd_rocclr"):
+            continue  # runtime copies
         key = (k, r["Counter_Name"])
         seen[key] = seen.get(key, 0) + 1
         if seen[key] <= skip_first:
