@@ -17,3 +17,10 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
       python3 bench.py --steps 10 --warmup 2 --batch $B --no-cpu-baseline $EXTRA > $OUT/p$i.log 2>&1 || exit $?
 done
+# LDS / scalar / instruction-issue detail (second set)
+for grp in "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU" \
+           "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SMEM_NORM"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
+      python3 bench.py --steps 10 --warmup 2 --batch $B --no-cpu-baseline $EXTRA > $OUT/p$i.log 2>&1 || { echo "group $grp failed"; }
+done
