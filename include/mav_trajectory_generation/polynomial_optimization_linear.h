@@ -129,19 +129,21 @@ class PolynomialOptimization {
     for (size_t v = 0; v < n_vertices_; ++v) {
       Vertex& vertex = vertices_[v];
       if (vertex.D() != (int)dimension_) fail(MTG_ERR_SIZE_MISMATCH, "vertex dimension mismatch");
-      bool valid = true;
-      Vertex tmp(dimension_);
-      for (auto it = vertex.cBegin(); it != vertex.cEnd(); ++it) {
-        if (it->first > kHighestDerivativeToOptimize) {
-          valid = false;
-          warn("Invalid constraint on vertex " + std::to_string(v) + ": maximum possible derivative is " +
-               std::to_string(kHighestDerivativeToOptimize) + ", but was set to " + std::to_string(it->first) +
-               ". Ignoring constraint");
-        } else {
-          tmp.addConstraint(it->first, it->second);
+      bool valid = true;  // (lin_impl:74-95; the vertex is rebuilt only when it must drop something)
+      for (auto it = vertex.cBegin(); it != vertex.cEnd(); ++it) valid = valid && it->first <= kHighestDerivativeToOptimize;
+      if (!valid) {
+        Vertex tmp(dimension_);
+        for (auto it = vertex.cBegin(); it != vertex.cEnd(); ++it) {
+          if (it->first > kHighestDerivativeToOptimize) {
+            warn("Invalid constraint on vertex " + std::to_string(v) + ": maximum possible derivative is " +
+                 std::to_string(kHighestDerivativeToOptimize) + ", but was set to " + std::to_string(it->first) +
+                 ". Ignoring constraint");
+          } else {
+            tmp.addConstraint(it->first, it->second);
+          }
         }
+        vertex = tmp;
       }
-      if (!valid) vertex = tmp;
     }
     updateSegmentTimes(segment_times);
     setupConstraintReorderingMatrix();
