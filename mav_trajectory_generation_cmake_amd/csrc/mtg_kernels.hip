@@ -302,13 +302,13 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
         if (valid) {
           double2* dst = reinterpret_cast<double2*>(a.coeffs + (pb * (K * D) + base) * N);
           const double2* src = reinterpret_cast<const double2*>(gst);
-          for (int e = c; e < nrun; e += LG) dst[e] = src[e];
+          for (int e = c; e < nrun; e += LG) store_stream(dst + e, src[e]);
         }
         __syncthreads();
       } else if (valid && have) {
         double2* dst = reinterpret_cast<double2*>(a.coeffs + ((pb * K + i) * D + dd) * N);
 #pragma unroll
-        for (int j = 0; j < N / 2; ++j) dst[j] = make_double2(out[2 * j], out[2 * j + 1]);
+        for (int j = 0; j < N / 2; ++j) store_stream(dst + j, make_double2(out[2 * j], out[2 * j + 1]));
       }
     }
     if (a.cost_out && have) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)

@@ -20,7 +20,8 @@ out = torch.empty((max(Bs), 10, 3, 10), dtype=torch.float64, device=dev)
 ctx = mtg.Context(0)
 for B in Bs:
     row = {"B": B}
-    for name, kw in (("lane", {"lane": True}), ("column", {})):
+    kinds = (("lane", {"lane": True}), ("column", {}))
+    for name, kw in [k for k in kinds if k[0] in os.environ.get("KERNELS", "lane,column").split(",")]:
         step = ctx.solve_call(10, 4, v_d[:B], m_d[:B], t_d[:B], out[:B], **kw)
         ctx.enable_timing(0)
         for _ in range(64):
@@ -30,4 +31,5 @@ for B in Bs:
             step()
         ms = ctx.kernel_times_ms(64)
         row[name] = round(float(np.mean(ms)) * 1e3, 2)
+    row["lib"] = os.environ.get("MTG_LIBRARY", "default")
     print(row, flush=True)
