@@ -28,6 +28,10 @@ constexpr size_t kMaxLdsHard = 160 * 1024;
 // HBM write latency once per round.
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Native 2 x f64 vector (HIP's double2 is a struct: arrays of it in registers can fall back to
+// private memory where a vector type stays in VGPRs).
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
 // Streaming (nontemporal) 16-B store of write-once output: `global_store_dwordx4 ... nt`.  The
 // coefficients are never re-read by the kernel; with plain stores they sat dirty in the XCDs' L2s
 // and drained at the end of the launch (config 2, B = 1e4: 18.8 -> 17.6 us with nt).
