@@ -520,6 +520,23 @@ def test_sharded_solves_bitwise_equal(gpu_ctx):
         np.testing.assert_array_equal(np.concatenate([a["cost"], b["cost"]]), whole["cost"])
 
 
+def test_output_only_8_byte_aligned(gpu_ctx):
+    """A device output array that is 8-B but not 16-B aligned takes the one-pass epilogue's 8-B
+    store loop: bit-equal to the 16-B path (B = 37: a partial last wave)."""
+    import torch
+    vals, mask, times = _bench_batch(37, seed0=5)
+    ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times)["coeffs"]
+    dev = torch.device("cuda", 0)
+    v_d, m_d, t_d = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (vals, mask, times))
+    buf = torch.full((ref.size + 1,), np.nan, dtype=torch.float64, device=dev)
+    out = buf[1:].view(ref.shape)
+    assert out.data_ptr() % 16 == 8
+    gpu_ctx.solve_call(10, 4, v_d, m_d, t_d, out)()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    assert np.isnan(buf[0].item())  # nothing written before the array
+
+
 def test_evaluate_range_long_clock_vs_oracle(gpu_ctx):
     """evaluateRange past the 128-run table (K = 30: ~300 runs, the rest resumed on the eval wave)
     and derivative orders outside the compile-time set (5, 7): bit-exact with the oracle."""
