@@ -207,8 +207,9 @@ def main():
     ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (configs 2, 4, 5: 1e4)")
     ap.add_argument("--segments", type=int, default=None)
     ap.add_argument("--N", type=int, default=None)
-    ap.add_argument("--timing-stride", type=int, default=16,
-                    help="time every n-th step's kernel with HIP events (1: every step)")
+    ap.add_argument("--timing-stride", type=int, default=0,
+                    help="also sample every n-th step's kernel with its own HIP event pair (0: none; the "
+                         "sampled launches add event overhead to the timed region)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -244,10 +245,13 @@ def main():
     m_d = torch.from_numpy(mask).to(dev)
     t_d = torch.from_numpy(times).to(dev)
     ctx = mtg.Context(local)
-    # Kernel time: every `timing_stride`-th step of the timed region goes through a second context
-    # that carries a HIP event pair in the kernel's dispatch packet.  Events on every launch cost
-    # ~4.5 us of GPU time per step at config 2 (22.3 -> 26.8 us per step, scripts/host_overhead.py),
-    # which would be charged to `value`; the sampled launches are the same kernel on the same stream.
+    # Kernel time (roofline): the HIP events g0 / g1 around the timed region on the launch stream;
+    # the launches run back to back (rocprofv3 shows no gap between them), so region time / steps is
+    # the kernel's steady-state duration.  Optionally (--timing-stride n) every n-th step goes through
+    # a second context that carries an event pair in the dispatch packet; events cost ~4.5 us of GPU
+    # time per launch at config 2 (scripts/host_overhead.py), charged to `value`, so this is off by
+    # default.  After the region, launches that each carry their own event pair give the duration of
+    # a launch that does not overlap its predecessor (reported as kernel_ms_isolated).
     ctx_t = mtg.Context(local)
     stream = torch.cuda.current_stream(dev)
     if wl == "config5":
@@ -272,11 +276,11 @@ def main():
         kflags = ((nat.MTG_FLAG_SPLIT_KERNELS if args.split else 0) | (nat.MTG_FLAG_GENERAL_KERNEL if args.general_kernel else 0)
                   | (nat.MTG_FLAG_LANE_KERNEL if args.lane_kernel else 0))
         kname = mtg._native.solve_kernel(N, D, K, r, kflags)
-    stride = max(1, args.timing_stride)
-    timed_steps = [i for i in range(args.steps) if i % stride == 0]
+    stride = args.timing_stride
+    timed_steps = [i for i in range(args.steps) if stride > 0 and i % stride == 0]
     ctx.enable_timing(0)
     ctx_t.enable_timing(max(len(timed_steps), 1))
-    plan = [step_t if i % stride == 0 else step for i in range(args.steps)]
+    plan = [step_t if stride > 0 and i % stride == 0 else step for i in range(args.steps)]
 
     for _ in range(args.warmup):
         step()
@@ -295,21 +299,17 @@ def main():
     el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    per_launch = ctx_t.kernel_times_ms(len(timed_steps))
+    per_launch = ctx_t.kernel_times_ms(len(timed_steps)) if timed_steps else np.zeros(0)
     gpu_ms = g0.elapsed_time(g1)
-    # Kernel duration for the roofline: launches that each carry their event pair, so consecutive
-    # kernels do not overlap (untimed).  Inside the timed region back-to-back launches do overlap: a
-    # sampled launch's start stamp is taken while the previous launch is still draining, so its
-    # event interval is LONGER than the per-step time (config 2: 20.1 us vs 18.8 us per step), i.e.
-    # it counts part of the previous kernel.  Both are reported; `kernel_ms` is the isolated one,
-    # which is what rocprofv3's kernel trace measures (profiles/).
+    kern_ms = gpu_ms / args.steps
+    # (A sampled launch's own event interval inside the region starts while its predecessor is still
+    # draining, so it reads longer than the per-step time: config 2, 20.1 vs 18.8 us.)
     n_iso = 32
     ctx_t.enable_timing(n_iso)
     for _ in range(n_iso):
         step_t()
     torch.cuda.synchronize(dev)
     iso = ctx_t.kernel_times_ms(n_iso)
-    kern_ms = float(np.mean(iso))
     el = max_over_ranks(el, dist if world > 1 else None, dev)
 
     # spot check of the timed outputs (finite) -- not timed
@@ -364,11 +364,12 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
                      "kernel": kname,
-                     "kernel_ms": kern_ms, "kernel_ms_method": "mean of %d launches, each with its own HIP event "
-                     "pair in the dispatch packet (no overlap with the previous launch)" % n_iso,
-                     "kernel_ms_min": float(np.min(iso)), "kernel_ms_max": float(np.max(iso)),
-                     "kernel_ms_in_stream": float(np.mean(per_launch)),
-                     "kernel_launches_in_stream": len(per_launch), "gpu_ms_timed_region": gpu_ms,
+                     "kernel_ms": kern_ms,
+                     "kernel_ms_method": "HIP events around the timed region on the launch stream / steps "
+                     "(back-to-back launches)",
+                     "kernel_ms_isolated": float(np.mean(iso)), "kernel_ms_isolated_min": float(np.min(iso)),
+                     "kernel_ms_sampled": float(np.mean(per_launch)) if len(per_launch) else None,
+                     "kernel_launches_sampled": len(per_launch), "gpu_ms_timed_region": gpu_ms,
                      "algorithmic_bytes_per_traj": bpt},
         "cpu_baseline": None,
     }
