@@ -10,13 +10,15 @@ OBJ=build/CMakeFiles/mav_trajectory_generation.dir/mav_trajectory_generation_cma
 OUT=mav_trajectory_generation_cmake_amd/lib_var/$name
 mkdir -p $OUT
 # the N = 10 kernel unit and the register kernels' host dispatch (LDS size), with the definitions
-for u in mtg_solve_reg_n10 mtg_solve_reg; do
+UNITS=${UNITS:-mtg_solve_reg_n10 mtg_solve_reg}  # (another kernel: UNITS="mtg_jacobian_n10")
+for u in $UNITS; do
   /opt/rocm/llvm/bin/clang++ -D__HIP_ROCclr__=1 -Dmav_trajectory_generation_EXPORTS -I include \
     -I mav_trajectory_generation_cmake_amd/csrc -O3 -DNDEBUG -std=gnu++17 --offload-arch=gfx950 -fPIC \
     -Wall -Wno-unused-parameter "$@" -o $OUT/$u.o -x hip -c mav_trajectory_generation_cmake_amd/csrc/$u.hip
 done
-objs=$(ls $OBJ/*.o | grep -v -e '/mtg_solve_reg_n10.hip.o$' -e '/mtg_solve_reg.hip.o$')
+excl=""; for u in $UNITS; do excl="$excl -e /$u.hip.o\$"; done
+objs=$(ls $OBJ/*.o | grep -v $excl)
 /opt/rocm/llvm/bin/clang++ -fPIC -O3 --offload-arch=gfx950 -shared --hip-link --rtlib=compiler-rt -unwindlib=libgcc \
-  -Wl,-soname,libmav_trajectory_generation.so -o $OUT/libmav_trajectory_generation.so $objs $OUT/mtg_solve_reg_n10.o $OUT/mtg_solve_reg.o
+  -Wl,-soname,libmav_trajectory_generation.so -o $OUT/libmav_trajectory_generation.so $objs $(for u in $UNITS; do echo $OUT/$u.o; done)
 rm -f $OUT/*.o
 echo built $OUT
