@@ -45,6 +45,8 @@ struct SolveArgs {
   int64_t B;              // trajectories (or trajectory x candidate pairs for the sweep)
   int K, D, r;
   int n_cand;             // candidates per trajectory for the sweep (1 for a plain solve)
+  int gi;                 // register column kernel: G in LDS for the interior-waypoint body (set by
+                          // launch_solve_reg, mtg_solve_reg.inc reg_gi_doubles)
 };
 
 // Lanes per trajectory and LDS bytes per workgroup for a shape; returns false

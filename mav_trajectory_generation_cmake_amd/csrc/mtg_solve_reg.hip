@@ -29,10 +29,45 @@ bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes) {
   return true;
 }
 
-hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream) {
+// G in LDS for the interior-waypoint body (reg_gi_doubles) shortens each wave's backward sweep but
+// takes LDS (config 2: 10.8 -> 15.0 KB per wave): use it when every wave of the launch is resident
+// at once under the larger footprint (config 2 at B = 1e4: 18.5 -> 17.7 us), not when the launch
+// runs in rounds (B = 131072: 157 -> 161 us, 12 -> 10 waves per CU).
+static bool use_gi(int N, const SolveArgs& a, int lg, size_t lds_plain, size_t* lds_gi) {
+  if (!kTwist || reg_gi_doubles(N, a.K, kTwist) == 0) return false;
+  const size_t bytes = (size_t)reg_lds_doubles(N, a.D, a.K, lg, kTwist, true) * sizeof(double);
+  if (bytes > kMaxLdsPerBlock || bytes == lds_plain) return false;
+  static int cus = -1, lds_cu = 0;
+  if (cus < 0) {
+    int dev = 0, c = 0, l = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&l, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+      c = 0;
+    lds_cu = l;
+    cus = c;
+  }
+  if (cus <= 0 || lds_cu <= 0) return false;
+  const int64_t tpb = kBlock / lg, waves = (a.B + tpb - 1) / tpb;
+  const size_t alloc = (bytes + 511) & ~(size_t)511;  // (LDS allocation granule)
+  int64_t per_cu = (int64_t)(lds_cu / alloc);
+  if (per_cu > 4 * MTG_REG_WAVES) per_cu = 4 * MTG_REG_WAVES;
+  if (waves > per_cu * cus) return false;
+  *lds_gi = bytes;
+  return true;
+}
+
+hipError_t launch_solve_reg(int N, const SolveArgs& a0, hipStream_t stream) {
   int lg;
   size_t lds;
-  if (!reg_geometry(N, a.D, a.K, &lg, &lds)) return hipErrorInvalidValue;
+  if (!reg_geometry(N, a0.D, a0.K, &lg, &lds)) return hipErrorInvalidValue;
+  SolveArgs a = a0;
+  a.gi = 0;
+  size_t lds_gi = 0;
+  if (use_gi(N, a, lg, lds, &lds_gi)) {
+    a.gi = 1;
+    lds = lds_gi;
+  }
   switch (N) {
     case 2: return launch_solve_reg_n2(a, lg, lds, stream);
     case 4: return launch_solve_reg_n4(a, lg, lds, stream);

@@ -520,6 +520,24 @@ def test_sharded_solves_bitwise_equal(gpu_ctx):
         np.testing.assert_array_equal(np.concatenate([a["cost"], b["cost"]]), whole["cost"])
 
 
+def test_g_in_lds_and_register_paths_bitwise_equal(gpu_ctx):
+    """The interior-waypoint body keeps G_v in LDS when a launch's waves are all resident (small
+    batches) and in registers otherwise (mtg_solve_reg.hip use_gi): the backward sweep does the same
+    arithmetic in the same order, so a trajectory's results are bit-identical either way."""
+    import torch
+    big = 40000  # 10000 waves in ONE launch (device pointers; host arrays this large go in chunks)
+    vals, mask, times = _bench_batch(big, seed0=901)
+    dev = torch.device("cuda", 0)
+    v_d, m_d, t_d = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (vals, mask, times))
+    c_d = torch.empty((big, 10, 3, 10), dtype=torch.float64, device=dev)
+    gpu_ctx.solve_call(10, 4, v_d, m_d, t_d, c_d)()
+    torch.cuda.synchronize()
+    whole = c_d.cpu().numpy()
+    part = gpu_ctx.solve_linear_batch(10, 4, vals[:777], mask[:777], times[:777])
+    np.testing.assert_array_equal(part["coeffs"], whole[:777])
+    np.testing.assert_array_equal(part["coeffs"][-1], whole[776])
+
+
 def test_output_only_8_byte_aligned(gpu_ctx):
     """A device output array that is 8-B but not 16-B aligned takes the one-pass epilogue's 8-B
     store loop: bit-equal to the 16-B path (B = 37: a partial last wave)."""
