@@ -36,25 +36,28 @@ bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes) {
 static bool use_gi(int N, const SolveArgs& a, int lg, size_t lds_plain, size_t* lds_gi) {
   if (!kTwist || reg_gi_doubles(N, a.K, kTwist) == 0) return false;
   const size_t bytes = (size_t)reg_lds_doubles(N, a.D, a.K, lg, kTwist, true) * sizeof(double);
-  if (bytes > kMaxLdsPerBlock || bytes == lds_plain) return false;
-  static int cus = -1, lds_cu = 0;
-  if (cus < 0) {
-    int dev = 0, c = 0, l = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+  if (bytes > kMaxLdsPerBlock) return false;
+  *lds_gi = bytes;
+  if (bytes == lds_plain) return true;  // (the G block fits the epilogue's staging area: free)
+  // the device's CU count and LDS per CU, cached per thread for its current device
+  thread_local int dev_cached = -1, cus = 0, lds_cu = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (dev != dev_cached) {
+    int c = 0, l = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipDeviceGetAttribute(&l, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
-      c = 0;
-    lds_cu = l;
+      return false;
+    dev_cached = dev;
     cus = c;
+    lds_cu = l;
   }
   if (cus <= 0 || lds_cu <= 0) return false;
   const int64_t tpb = kBlock / lg, waves = (a.B + tpb - 1) / tpb;
   const size_t alloc = (bytes + 511) & ~(size_t)511;  // (LDS allocation granule)
   int64_t per_cu = (int64_t)(lds_cu / alloc);
   if (per_cu > 4 * MTG_REG_WAVES) per_cu = 4 * MTG_REG_WAVES;
-  if (waves > per_cu * cus) return false;
-  *lds_gi = bytes;
-  return true;
+  return waves <= per_cu * cus;
 }
 
 hipError_t launch_solve_reg(int N, const SolveArgs& a0, hipStream_t stream) {
