@@ -21,9 +21,9 @@
 // polynomials use the reference's Horner form (Polynomial::evaluate,
 // polynomial.h:138-151), multiply-then-add.
 #include <float.h>
+#include <stdlib.h>
 
-#include "mtg_internal.h"
-#include "mtg_tables.inc"
+#include "mtg_device.h"
 
 namespace mtg {
 
@@ -233,7 +233,8 @@ struct RunHead {
 
 // The clock, one thread per trajectory, writing its first `cap` runs to the run table.  The clock
 // is a serial chain per trajectory; run here, 64 trajectories share a wave's lanes, where the eval
-// kernel's lane 0 would run it alone while its wave waits.
+// kernel's lane 0 would run it alone while its wave waits.  (16 or 32 trajectories per wave, i.e.
+// 4x / 2x the waves, measured slower: count 0.155 -> 0.205 / 0.166 ms at 1e4, scripts/eval_ab_env.sh.)
 __global__ void eval_runs_kernel(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
                                  int cap, RunHead* heads, RunRec* runs) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -284,8 +285,10 @@ struct RunLds {  // structure of arrays in LDS
 // evaluate the runs' samples -- consecutive samples on consecutive lanes -- with the coefficients
 // staged in LDS.
 // DER >= 0: the derivative order at compile time (0..4, the common ones); DER < 0: `derivative`.
-template <int N, int DER>
-__global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, const double* coeffs,
+// DD > 0: D at compile time (the sample loop takes kSpl samples per lane per block); 0: D at run time.
+constexpr int kSpl = 2;
+template <int N, int DER, int DD>
+__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3))) void eval_range_kernel(int D, int K, const double* coeffs,
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
@@ -379,6 +382,113 @@ __global__ __launch_bounds__(kEvalThreads) void eval_range_kernel(int D, int K, 
     if (nr == 0) break;
     const int64_t first = rt->n0[0], end = s_end < n_total ? s_end : n_total;
     int ri = 0;
+    if constexpr (DD > 0) {
+      // D at compile time: each lane takes kSpl samples per block (n = nb + s 64 + lane), and their
+      // kSpl D Horner chains are independent, so they interleave instead of running one dimension
+      // after the other; the staged rows are read back in one batch before the stores.
+      constexpr int kBlk = kSpl * kEvalThreads;
+      int64_t nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;  // the next run's first sample
+      double cc[DD * N];  // the cached segment's Horner terms (wave-uniform)
+      int cseg = -1;
+      for (int64_t nb = first; nb < end; nb += kBlk) {
+        const int cnt = (int)(end - nb < kBlk ? end - nb : kBlk);
+        double tv[kSpl];
+        const double* cs[kSpl];
+        int sg[kSpl];
+#pragma unroll
+        for (int s = 0; s < kSpl; ++s) {
+          const int64_t n = nb + s * kEvalThreads + lane;
+          const bool have = n < end;
+          while (have && nxt <= n) {
+            ++ri;
+            nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;
+          }
+          const int64_t k = n - rt->n0[ri];
+          double t, a;
+          if (rt->single[ri]) {
+            t = rt->tin0[ri];
+            a = rt->acc0[ri];
+          } else {
+            t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
+            a = sample_times ? mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]) : 0.0;
+          }
+          tv[s] = t;
+          sg[s] = rt->seg[ri];
+          cs[s] = cf + (sg[s] * DD) * N;
+          if (sample_times && have) sample_times[base + n] = a;
+        }
+        double v[kSpl][DD];
+        // Usually the whole block lies in one segment (a segment has ~750 samples at dt = 0.01): its
+        // coefficients then come from registers, reloaded from LDS only when the wave's segment
+        // changes.  Per-lane LDS reads of every coefficient for every sample made the CU's LDS
+        // bandwidth the limit (~30 16-B reads per lane per block).
+        const int sg0 = __builtin_amdgcn_readfirstlane(sg[0]);
+        bool same = true;
+#pragma unroll
+        for (int s = 0; s < kSpl; ++s) same = same && sg[s] == sg0;
+        if (__builtin_amdgcn_ballot_w64(!same) == 0) {
+          if (sg0 != cseg) {
+            const double* c0 = cf + (sg0 * DD) * N;
+#pragma unroll
+            for (int i = 0; i < DD * N; ++i) cc[i] = c0[i];
+            cseg = sg0;
+          }
+#pragma unroll
+          for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+            for (int d = 0; d < DD; ++d) v[s][d] = derivative < N ? cc[d * N + N - 1] : 0.0;
+          if (derivative < N) {
+#pragma unroll
+            for (int j = N - 2; j >= 0; --j) {
+              if (DER >= 0 ? j >= DER : j >= derivative) {
+#pragma unroll
+                for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+                  for (int d = 0; d < DD; ++d) {
+                    v[s][d] = v[s][d] * tv[s];
+                    v[s][d] = v[s][d] + cc[d * N + j];
+                  }
+              }
+            }
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+            for (int d = 0; d < DD; ++d) v[s][d] = derivative < N ? cs[s][d * N + N - 1] : 0.0;
+          if (derivative < N) {
+#pragma unroll
+            for (int j = N - 2; j >= 0; --j) {
+              if (DER >= 0 ? j >= DER : j >= derivative) {
+#pragma unroll
+                for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+                  for (int d = 0; d < DD; ++d) {
+                    v[s][d] = v[s][d] * tv[s];
+                    v[s][d] = v[s][d] + cs[s][d * N + j];
+                  }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+          for (int d = 0; d < DD; ++d) ob[(s * kEvalThreads + lane) * DD + d] = v[s][d];
+        lds_fence();  // one wave per block: the staged rows are complete
+        double* dst = out + (base + nb) * DD;
+        double w[kSpl * DD];
+#pragma unroll
+        for (int u = 0; u < kSpl * DD; ++u) w[u] = ob[u * kEvalThreads + lane];
+        lds_fence();  // (read before the next block overwrites them)
+#pragma unroll
+        for (int u = 0; u < kSpl * DD; ++u)
+          if (u * kEvalThreads + lane < cnt * DD) dst[u * kEvalThreads + lane] = w[u];
+      }
+      if (end >= n_total) break;
+      __syncthreads();  // the run table is refilled next
+      continue;
+    }
     for (int64_t nb = first; nb < end; nb += kEvalThreads) {
       const int64_t n = nb + lane;
       const int cnt = (int)(end - nb < kEvalThreads ? end - nb : kEvalThreads);
@@ -458,11 +568,23 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
     launch_kernel(eval_runs_kernel, dim3((unsigned)((B + block - 1) / block)), dim3(block), 0, stream, K, B, times,
                   t_start, t_end, dt, cap, heads, runs);
   }
-  const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)kEvalThreads * D);
+  // D = 3 (every reference problem in 3-D) has its own kernels: the sample loop's dimensions unrolled
+  const bool d3 = D == 3;
+  // One block per trajectory.  (Splitting a trajectory's samples over 2 or 4 blocks, to shorten the
+  // launch's tail, measured slower at 1e4 config-2 trajectories: 0.795 -> 0.80 / 0.855 ms; every
+  // block reloads the run table and stages the coefficients.)
+  const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)(d3 ? kSpl : 1) * kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
-#define MTG_EVAL_LAUNCH(NN, DD)                                                                          \
-  launch_kernel(eval_range_kernel<NN, DD>, dim3((unsigned)B), dim3(kEvalThreads), lds, stream, D, K, coeffs, \
-                times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs)
+  const dim3 grid((unsigned)B);
+#define MTG_EVAL_LAUNCH(NN, DER)                                                                                   \
+  do {                                                                                                             \
+    if (d3)                                                                                                        \
+      launch_kernel(eval_range_kernel<NN, DER, 3>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
+                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs);  \
+    else                                                                                                           \
+      launch_kernel(eval_range_kernel<NN, DER, 0>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
+                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs);  \
+  } while (0)
 #define MTG_EVAL_CASE(NN)                 \
   case NN:                                \
     switch (derivative) {                 \

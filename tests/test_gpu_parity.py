@@ -219,9 +219,9 @@ def test_paths_agree_mixed_masks(gpu_ctx):
 
 @pytest.mark.parametrize("K", [13, 17, 20])
 def test_wide_register_bucket_n12(gpu_ctx, K):
-    """N = 12, 12 < K <= 20 (config 4's shape) runs the register kernel's wide bucket (KMAX 20, one
-    wave per SIMD): against the general LDS-resident kernel and the oracle, with waypoint masks
-    (the IP fast path at K = 20) and with per-trajectory extra fixed derivatives (dense path)."""
+    """N = 12, 12 < K <= 20 (config 4's shape) runs the register kernel's wide bucket (KMAX 20, G_v in
+    LDS, two waves per SIMD): against the general LDS-resident kernel and the oracle, with waypoint
+    masks (the IP fast path at K = 20) and with per-trajectory extra fixed derivatives (dense path)."""
     O = _oracle()
     from mav_trajectory_generation_cmake_amd import random_vertices_batch
     B = 37  # ragged: 4 trajectories per wave
@@ -250,9 +250,9 @@ def test_wide_register_bucket_n12(gpu_ctx, K):
 @pytest.mark.parametrize("K", [13, 20])
 @pytest.mark.parametrize("D", [1, 2, 3, 4, 6, 11])
 def test_wide_register_bucket_n12_dimensions(gpu_ctx, D, K):
-    """The wide bucket parks G_v, v >= 10, on lanes 9..14 of each trajectory's lane group, so the
-    group needs 16 lanes even where H + D <= 8 (D = 1, 2: a yaw or planar problem), and for
-    D >= 4 those lanes are dimension lanes too; D = 11 takes a 32-lane group.  Against the general
+    """The wide bucket across dimension counts: D = 1, 2 (a yaw or planar problem, H + D <= 8 lanes
+    per chain), D = 3, 4, 6 and D = 11 (a 32-lane group); round 1's layout parked G_v on lanes 9..14
+    and broke where the group had fewer lanes, so every D is checked (G_v now lives in LDS).  Against the general
     LDS-resident kernel (1e-9) and the oracle, with waypoint masks and with mixed masks."""
     O = _oracle()
     B = 21
