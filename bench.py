@@ -377,7 +377,7 @@ def main():
     # D2H, synchronize -- the PCIe-inclusive rate of a caller that holds its batch in host memory
     if wl != "config5":
         out["end_to_end"] = end_to_end(ctx, N, r, values, mask, times, unit, bpt - K * D * N * 8, K * D * N * 8)
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (the CPU baseline is an N = 1 figure)
         host = host_cpu_info()
         threads = int(os.environ.get("MTG_CPU_THREADS", host["usable_cpus"]))
         S = min(args.cpu_sample, B)

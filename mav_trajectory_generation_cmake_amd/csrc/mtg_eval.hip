@@ -21,7 +21,6 @@
 // polynomials use the reference's Horner form (Polynomial::evaluate,
 // polynomial.h:138-151), multiply-then-add.
 #include <float.h>
-#include <stdlib.h>
 
 #include "mtg_device.h"
 
