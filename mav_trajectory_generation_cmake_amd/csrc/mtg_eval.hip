@@ -547,7 +547,10 @@ size_t eval_workspace_bytes(int K, int64_t B, int* cap) {
   // the samples it describes at 128 and is capped at 2 GB; a trajectory with more runs than the
   // table holds continues on its eval wave's lane 0
   (void)K;
-  int c = 128;
+#ifndef MTG_EVAL_RUN_CAP
+#define MTG_EVAL_RUN_CAP 128
+#endif
+  int c = MTG_EVAL_RUN_CAP;
   while (c > 8 && (double)B * (c * sizeof(RunRec) + sizeof(RunHead)) > 2.0e9) c /= 2;
   *cap = c;
   return (size_t)B * (sizeof(RunHead) + (size_t)c * sizeof(RunRec));
