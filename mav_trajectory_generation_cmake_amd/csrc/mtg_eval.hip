@@ -534,7 +534,7 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
                              double t_end, double dt, int64_t* counts, hipStream_t stream) {
   (void)N;
   (void)D;
-  const int block = 256;
+  const int block = 64;  // (256-thread blocks put the 1e4 clocks of config 2 on 40 CUs: 0.163 -> 0.154 ms)
   const int64_t grid = (B + block - 1) / block;
   if (grid == 0) return hipSuccess;
   launch_kernel(eval_count_kernel, dim3((unsigned)grid), dim3(block), 0, stream, K, B, times, t_start,
@@ -543,14 +543,12 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
 }
 
 size_t eval_workspace_bytes(int K, int64_t B, int* cap) {
-  // up to 128 runs per trajectory (config 2 has ~100), fewer for huge batches: the table is ~4% of
-  // the samples it describes at 128 and is capped at 2 GB; a trajectory with more runs than the
+  // up to 256 runs per trajectory (config 2 has ~100-130: at 128 some trajectories overflowed to
+  // the slow path, 0.793 -> 0.785 ms at 1e4), fewer for huge batches: the table is only written as
+  // far as each trajectory's runs go and is capped at 2 GB; a trajectory with more runs than the
   // table holds continues on its eval wave's lane 0
   (void)K;
-#ifndef MTG_EVAL_RUN_CAP
-#define MTG_EVAL_RUN_CAP 128
-#endif
-  int c = MTG_EVAL_RUN_CAP;
+  int c = 256;
   while (c > 8 && (double)B * (c * sizeof(RunRec) + sizeof(RunHead)) > 2.0e9) c /= 2;
   *cap = c;
   return (size_t)B * (sizeof(RunHead) + (size_t)c * sizeof(RunRec));
