@@ -60,12 +60,13 @@ def shard_seed0(rank, batch_per_rank):
     return rank * batch_per_rank
 
 
-def max_over_ranks(x, dist, device):
-    """Slowest rank's elapsed time (the job's wall clock); identity at world size 1."""
+def max_over_ranks(x, dist):
+    """Slowest rank's elapsed time (the job's wall clock); identity at world size 1.  A host-side
+    MAX over the gloo group (the only cross-rank step is this scalar)."""
     import torch
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return float(x)
-    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(x)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -203,6 +204,9 @@ def main():
     # kernel at 195 us instead of 155 us), and a timed region of ~15 ms at config 2
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--min-warmup-ms", type=float, default=300.0,
+                    help="keep warming up until this much wall time has passed, whatever --warmup is (the "
+                         "GPU clocks settle over ~100 ms of back-to-back launches)")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2")
     ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (configs 2, 4, 5: 1e4)")
     ap.add_argument("--segments", type=int, default=None)
@@ -227,7 +231,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        # gloo: the ranks exchange only a barrier and one scalar (no data-path collective), so the
+        # multi-GPU run does not depend on RCCL
+        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -282,8 +288,14 @@ def main():
     ctx_t.enable_timing(max(len(timed_steps), 1))
     plan = [step_t if stride > 0 and i % stride == 0 else step for i in range(args.steps)]
 
-    for _ in range(args.warmup):
-        step()
+    # warmup: at least --warmup steps AND at least --min-warmup-ms of wall time
+    w0 = time.perf_counter()
+    warm = 0
+    while warm < args.warmup or (time.perf_counter() - w0) * 1e3 < args.min_warmup_ms:
+        for _ in range(max(1, min(args.warmup, 100))):
+            step()
+            warm += 1
+        torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -310,7 +322,7 @@ def main():
         step_t()
     torch.cuda.synchronize(dev)
     iso = ctx_t.kernel_times_ms(n_iso)
-    el = max_over_ranks(el, dist if world > 1 else None, dev)
+    el = max_over_ranks(el, dist if world > 1 else None)
 
     # spot check of the timed outputs (finite) -- not timed
     assert np.isfinite(out_d.cpu().numpy()).all(), "non-finite outputs"
@@ -352,6 +364,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_steps_run": warm,
         "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

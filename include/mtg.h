@@ -61,8 +61,10 @@ extern "C" {
 
 /* Per-trajectory status bits (status[b]). */
 #define MTG_TRAJ_OK 0
-#define MTG_TRAJ_BAD_TIME 1            /* some T <= 0, < DBL_EPSILON or not finite (CHECK_GT lin_impl:287) */
-#define MTG_TRAJ_NOT_SPD 2             /* non-positive pivot in R_pp (reference: undetected, lin_impl:355-368) */
+#define MTG_TRAJ_BAD_TIME 1            /* some T <= 0 or not finite (CHECK_GT lin_impl:287) */
+#define MTG_TRAJ_NOT_SPD 2             /* non-positive pivot in R_pp (reference: undetected, lin_impl:355-368),
+                                          or some 0 < T < DBL_EPSILON, where the reference's A(T) is
+                                          singular (baseCoeffsWithTime, polynomial.h:225) */
 #define MTG_TRAJ_WARN_DROPPED 256      /* constraint of order > N/2-1 ignored (LOG(WARNING) lin_impl:84-87) */
 #define MTG_TRAJ_ERROR_MASK 255
 
@@ -72,8 +74,8 @@ extern "C" {
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
 #define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
                                           (default: see mtg_solve_kernel) */
-#define MTG_FLAG_LANE_KERNEL 16u       /* the lane-per-chain kernel where it applies (N in {6, 8, 10},
-                                          D <= 4, K <= 10; a fifth of the default kernel's
+#define MTG_FLAG_LANE_KERNEL 16u       /* the lane-per-chain kernel where it applies (N in {6, 8} with
+                                          K <= 12, N = 10 with K <= 10; D <= 4; a fifth of the default kernel's
                                           instructions per trajectory, but latency-bound at one wave
                                           per SIMD: DESIGN.md 3.2) */
 

@@ -185,6 +185,8 @@ void destroy_pipe(mtg_ctx* ctx) {
 
 // host-pointer solves above this size go through the chunked pipeline
 constexpr size_t kPipelineMinBytes = 8u << 20;
+// returned by run_solve_pipelined when it could not start its D2H thread (nothing was issued)
+constexpr int kPipelineUnavailable = 1;
 
 // Host-pointer batch solve as a pipeline of chunks (the reference's equivalent is a
 // loop of single solves, src/polynomial_timing_evaluation.cpp:119-126).  Each of kPipeSlots slots
@@ -222,9 +224,6 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
   const size_t o_status = off; off = align_up(off + s_status * chunk);
   MTG_HIP_TRY(ctx, ensure_pipe(ctx));
   for (auto& s : ctx->pipe) MTG_HIP_TRY(ctx, ensure(&s.dev, &s.dev_bytes, off));
-  // order after whatever the caller queued on the context's stream
-  MTG_HIP_TRY(ctx, hipEventRecord(ctx->pipe_start, ctx->stream));
-  for (auto& s : ctx->pipe) MTG_HIP_TRY(ctx, hipStreamWaitEvent(s.stream, ctx->pipe_start, 0));
 
   std::mutex m;
   std::condition_variable cv;
@@ -238,7 +237,7 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
   };
   // D2H issuer: chunk c's outputs into the caller's arrays, on the chunk's slot stream (ordered after
   // its kernel), then wait for them and retire the chunk
-  std::thread d2h([&] {
+  auto d2h_body = [&] {
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return fail(e, "hipSetDevice");
     for (int64_t c = 0; c < n_chunks; ++c) {
@@ -269,7 +268,22 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       retired = c + 1 == n_chunks ? n_chunks : c;
       cv.notify_all();
     }
-  });
+  };
+  std::thread d2h;
+  try {
+    d2h = std::thread(d2h_body);
+  } catch (...) {  // no thread (std::system_error): nothing was issued, the caller stages instead
+    return kPipelineUnavailable;
+  }
+  {
+    // the pipeline's whole span (every chunk's H2D, kernel and D2H) is this call's timed interval;
+    // the slot streams start after whatever the caller queued on the context's stream
+    hipError_t e = time_begin(ctx, false);
+    if (e == hipSuccess) e = hipEventRecord(ctx->pipe_start, ctx->stream);
+    for (auto& s : ctx->pipe)
+      if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, ctx->pipe_start, 0);
+    if (e != hipSuccess) fail(e, "pipeline start");
+  }
   // H2D + kernel issuer (this thread)
   for (int64_t c = 0; c < n_chunks; ++c) {
     {
@@ -316,6 +330,13 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
   d2h.join();
   for (auto& s : ctx->pipe) (void)hipStreamSynchronize(s.stream);  // nothing may still read the caller's arrays
   if (err != hipSuccess) return set_hip_error(ctx, err, err_what);
+  // close the timed interval after the last D2H of every slot
+  for (auto& s : ctx->pipe) {
+    MTG_HIP_TRY(ctx, hipEventRecord(s.done, s.stream));
+    MTG_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, s.done, 0));
+  }
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return MTG_OK;
 }
 
@@ -327,10 +348,13 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   const int V = K + 1, h = N / 2;
   const int64_t pairs = batch * n_cand;
   MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
-  if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 &&
-      (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes)
-    return run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out, cost_out,
-                               status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL));
+  // (a time sweep passes scales, also with one candidate: it takes the single-stream path, which stages them)
+  if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 && !scales &&
+      (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes) {
+    const int rc = run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out,
+                                       cost_out, status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL));
+    if (rc != kPipelineUnavailable) return rc;
+  }
   mtg::SolveArgs a{};
   a.B = pairs;
   a.K = K;

@@ -63,7 +63,13 @@ __device__ __forceinline__ void seg_powers(double T, double (&s)[H], double& sc)
   }
 }
 
-__device__ __forceinline__ bool time_ok(double T) { return T >= DBL_EPSILON && T <= DBL_MAX; }
+// Status bits of one segment time.  T must be > 0 and finite (CHECK_GT(segment_time, 0), lin_impl:287):
+// otherwise BAD_TIME.  For 0 < T < DBL_EPSILON the reference's baseCoeffsWithTime keeps only the
+// t = 0 entry (polynomial.h:225), so its mapping matrix A(T) is singular and its solve is not
+// defined: reported as NOT_SPD, not as a bad time.
+__device__ __forceinline__ int time_bits(double T) {
+  return !(T > 0.0 && T <= DBL_MAX) ? MTG_TRAJ_BAD_TIME : (T < DBL_EPSILON ? MTG_TRAJ_NOT_SPD : 0);
+}
 
 template <int H>
 __device__ __forceinline__ void load_fixed(const double* vals, int v, int D, int d, unsigned m,

@@ -36,7 +36,14 @@ namespace {
 const double kA1inv[MTG_A1INV_SIZE] = {MTG_A1INV_VALUES};
 const double kHtilde[MTG_HTILDE_SIZE] = {MTG_HTILDE_VALUES};
 
-inline bool time_ok(double T) { return T >= DBL_EPSILON && T <= DBL_MAX; }
+// T > 0 and finite (CHECK_GT(segment_time, 0), lin_impl:287)
+inline bool time_ok(double T) { return T > 0.0 && T <= DBL_MAX; }
+// Status bits of one segment time: BAD_TIME for T <= 0 or not finite; for 0 < T < DBL_EPSILON the
+// reference's A(T) is singular (baseCoeffsWithTime keeps only the t = 0 entry, polynomial.h:225), so
+// its solve is undefined there: NOT_SPD.
+inline int32_t time_bits(double T) {
+  return !time_ok(T) ? MTG_TRAJ_BAD_TIME : (T < DBL_EPSILON ? MTG_TRAJ_NOT_SPD : 0);
+}
 
 // Per-thread working storage of one trajectory (sized for the largest call seen).
 struct Scratch {
@@ -177,7 +184,7 @@ struct HostSolve {
     // (H_i [1 0..0 1 0..0]^T = 0), which removes the cancellation of H^TL p_i + H^TR p_i+1
     for (int i = 0; i < K; ++i) {
       const double T = times[i];
-      if (!time_ok(T)) st |= MTG_TRAJ_BAD_TIME;  // CHECK_GT(segment_time, 0) (lin_impl:287)
+      st |= time_bits(T);  // CHECK_GT(segment_time, 0) (lin_impl:287)
       double* s = PW + (size_t)i * H;
       s[0] = 1.0;
       for (int k = 1; k < H; ++k) s[k] = s[k - 1] * T;

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
   for (int k = 0; k < H; ++k) sp[k] = 0.0;
   {
     const double T0 = tms[0] * tscale;
-    if (!time_ok(T0)) st |= MTG_TRAJ_BAD_TIME;
+    st |= time_bits(T0);
     seg_powers<H, R>(T0, sn, scn);
   }
   unsigned raw = msk[0];
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg
       m_cur = m_next;
       if (v + 1 < K) {
         const double Tn = tms[v + 1] * tscale;
-        if (!time_ok(Tn)) st |= MTG_TRAJ_BAD_TIME;
+        st |= time_bits(Tn);
         seg_powers<H, R>(Tn, sn, scn);
         raw = msk[v + 2];
         if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;

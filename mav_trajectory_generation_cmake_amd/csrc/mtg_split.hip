@@ -146,7 +146,7 @@ __global__ __launch_bounds__(128) void block_cholesky_kernel(SolveArgs a, double
     const unsigned raw = msk[v];
     if (raw & ~HM) st |= MTG_TRAJ_WARN_DROPPED;
     n_free += __builtin_popcount(~raw & HM);
-    if (v < K && !time_ok(tms[v] * tscale)) st |= MTG_TRAJ_BAD_TIME;
+    if (v < K) st |= time_bits(tms[v] * tscale);
   }
 
   // forward: S_v = D_v - E_{v-1}^T G_{v-1}, rhs_v = b_v - E_{v-1}^T z_{v-1}; factor; G_v, z_v

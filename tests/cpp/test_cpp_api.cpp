@@ -31,6 +31,18 @@ static int g_fail = 0;
     }                                                           \
   } while (0)
 
+// v << a, b (, c): the Eigen comma initializer, valid with Eigen and with the drop-in's own types
+static VectorXd vec(double a, double b) {
+  VectorXd v(2);
+  v << a, b;
+  return v;
+}
+static VectorXd vec(double a, double b, double c) {
+  VectorXd v(3);
+  v << a, b, c;
+  return v;
+}
+
 static double maxabs(const VectorXd& v) {
   double m = 0;
   for (int i = 0; i < (int)v.size(); ++i) m = std::fmax(m, std::fabs(v[i]));
@@ -102,7 +114,7 @@ static void test_mapping_matrix_inversion() {
       for (int j = 0; j < 10; ++j) err = std::fmax(err, std::fabs(P(i, j) - (i == j ? 1.0 : 0.0)));
     EXPECT(err < 1e-10 * std::pow(T, 9), "A^-1 A != I at T=%g (%g)", T, err);
   }
-  Vertex::Vector vertices = createRandomVertices(derivative_order::SNAP, 4, VectorXd{-1, -1}, VectorXd{1, 1}, 3);
+  Vertex::Vector vertices = createRandomVertices(derivative_order::SNAP, 4, vec(-1.0, -1.0), vec(1.0, 1.0), 3);
   const std::vector<double> times = estimateSegmentTimes(vertices, 3.0, 5.0);
   PolynomialOptimization<10> opt(2);
   opt.setupFromVertices(vertices, times);
@@ -187,9 +199,9 @@ static void test_constraint_packing() {
   for (int v = 0; v <= K; ++v) {
     Vertex vx(D);
     if (v == 0 || v == K)
-      vx.makeStartOrEnd(VectorXd{1.0 * v, 2.0, 3.0}, derivative_order::JERK);
+      vx.makeStartOrEnd(vec(1.0 * v, 2.0, 3.0), derivative_order::JERK);
     else
-      vx.addConstraint(derivative_order::POSITION, VectorXd{1.0 * v, -1.0 * v, 0.5 * v});
+      vx.addConstraint(derivative_order::POSITION, vec(1.0 * v, -1.0 * v, 0.5 * v));
     vertices.push_back(vx);
   }
   PolynomialOptimization<10> opt(D);
@@ -220,9 +232,9 @@ static void test_evaluate_range(bool device) {
   for (int v = 0; v <= 3; ++v) {
     Vertex vx(2);
     if (v == 0 || v == 3)
-      vx.makeStartOrEnd(VectorXd{1.0 * v, -2.0 * v}, derivative_order::SNAP);
+      vx.makeStartOrEnd(vec(1.0 * v, -2.0 * v), derivative_order::SNAP);
     else
-      vx.addConstraint(derivative_order::POSITION, VectorXd{1.0 * v + 0.3, 0.7 * v});
+      vx.addConstraint(derivative_order::POSITION, vec(1.0 * v + 0.3, 0.7 * v));
     vertices.push_back(vx);
   }
   PolynomialOptimization<10> opt(2);
@@ -308,9 +320,9 @@ static void test_free_constraints_and_reparametrisation() {
   for (int v = 0; v <= K; ++v) {
     Vertex vx(D);
     if (v == 0 || v == K)
-      vx.makeStartOrEnd(VectorXd{1.0 * v, 2.0 - v, 0.5}, derivative_order::SNAP);
+      vx.makeStartOrEnd(vec(1.0 * v, 2.0 - v, 0.5), derivative_order::SNAP);
     else
-      vx.addConstraint(derivative_order::POSITION, VectorXd{1.0 * v + 0.2 * (v % 2), -0.7 * v, 0.3 * v * v});
+      vx.addConstraint(derivative_order::POSITION, vec(1.0 * v + 0.2 * (v % 2), -0.7 * v, 0.3 * v * v));
     vertices.push_back(vx);
   }
   std::vector<double> times{1.1, 0.8, 1.7, 2.2, 0.9, 1.3};
@@ -355,8 +367,8 @@ static void test_free_constraints_and_reparametrisation() {
 // The matrices of one fixed problem, for tests/test_cpp_api.py to compare with the oracle's.
 static int dump(const char* path) {
   Vertex::Vector vertices =
-      createRandomVertices(derivative_order::SNAP, 5, VectorXd{-10, -20, -10}, VectorXd{10, 20, 10}, 12345);
-  vertices[2].addConstraint(derivative_order::VELOCITY, VectorXd{0.5, -0.25, 1.0});  // a mixed mask
+      createRandomVertices(derivative_order::SNAP, 5, vec(-10.0, -20.0, -10.0), vec(10.0, 20.0, 10.0), 12345);
+  vertices[2].addConstraint(derivative_order::VELOCITY, vec(0.5, -0.25, 1.0));  // a mixed mask
   const std::vector<double> times = estimateSegmentTimes(vertices, 3.0, 5.0);
   PolynomialOptimization<10> opt(3);
   opt.setupFromVertices(vertices, times, derivative_order::SNAP);

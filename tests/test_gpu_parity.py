@@ -152,6 +152,10 @@ def test_status_codes(gpu_ctx):
     out = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True)
     assert out["status"][0] == 0
     assert all(out["status"][i] & nat.MTG_TRAJ_BAD_TIME for i in (1, 2, 3))
+    t2 = times[:1].copy()
+    t2[0, 4] = 1e-17  # > 0 but the reference's A(T) is singular (polynomial.h:225): NOT_SPD, as on the host
+    tiny = gpu_ctx.solve_linear_batch(10, 4, vals[:1], mask[:1], t2, status=True)["status"][0]
+    assert tiny & nat.MTG_TRAJ_NOT_SPD and not tiny & nat.MTG_TRAJ_BAD_TIME, tiny
     with pytest.raises(nat.MTGError) as e:
         gpu_ctx.solve_linear_batch(10, 5, vals, mask, times)
     assert e.value.code == nat.MTG_ERR_BAD_DERIVATIVE
@@ -684,3 +688,45 @@ def test_pipelined_host_arrays(gpu_ctx, pinned):
         host = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, free=True, n_free=True, cost=True, status=True)
     for k in ("coeffs", "free", "n_free", "cost", "status"):
         np.testing.assert_array_equal(host[k], dev[k].cpu().numpy(), err_msg=k)
+
+
+def test_time_sweep_one_candidate_large_host_batch(gpu_ctx):
+    """A time sweep with ONE candidate on host arrays large enough for the pipelined solve path must
+    still apply the scale: cost == computeCost of solves at scale * times (nl_impl:765-832).  A
+    pipelined plain solve of the same batch records its span in the timing ring."""
+    B = 6000
+    vals, mask, times = _bench_batch(B, seed0=4242)
+    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, np.array([1.37]))
+    ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times * 1.37, cost=True)["cost"]
+    np.testing.assert_allclose(J[:, 0], ref, rtol=1e-12, atol=0)
+    unscaled = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, cost=True)["cost"]
+    assert np.all(np.abs(J[:, 0] - unscaled) > 1e-6 * unscaled)
+    gpu_ctx.enable_timing(4)
+    gpu_ctx.solve_linear_batch(10, 4, vals, mask, times)  # 8.3 MB of host arrays: pipelined
+    ms = gpu_ctx.kernel_times_ms(4)
+    assert len(ms) == 1 and ms[0] > 0.0, ms
+    gpu_ctx.enable_timing(1)
+
+
+def test_config5_full_size_vs_oracle(gpu_ctx):
+    """BASELINE config 5 at the bench's exact size and tiles: 1e4 config-2 trajectories x 64 candidate
+    allocations T_c = (0.5 + c/63) T (bench.py), the cost J(b, c) and the exact time Jacobian on the
+    matrix cores.  A random sample of 256 trajectories against the oracle's reference-algorithm J and
+    Richardson-limit Jacobian (getCostAndGradientTime's J_d part, nl_impl:2155-2243); the VALU
+    cost_at_times kernel against the whole batch."""
+    O = _oracle()
+    N, r, K, B, C = 10, 4, 10, 10000, 64
+    vals, mask, times = _bench_batch(B, seed0=0)
+    xf, _ = _solved_full_values(gpu_ctx, N, r, vals, mask, times)
+    scales = np.repeat((0.5 + np.arange(C) / (C - 1.0))[:, None], K, axis=1)
+    J, G = gpu_ctx.time_jacobian_batch(N, r, xf, times, scales)
+    assert J.shape == (B, C) and G.shape == (B, C, K)
+    assert np.all(np.isfinite(J)) and np.all(np.isfinite(G))
+    Jc = gpu_ctx.cost_at_times_batch(N, r, xf, times, scales)
+    np.testing.assert_allclose(J, Jc, rtol=1e-11, atol=0)
+    rng = np.random.default_rng(55)
+    sel = np.sort(rng.choice(B, 256, replace=False))
+    Jr, Gr = O.cost_time_jacobian_batch(N, r, xf[sel], times[sel], scales, 0.0)
+    np.testing.assert_allclose(J[sel], Jr, rtol=1e-7, atol=0)
+    gscale = np.max(np.abs(Gr), axis=2, keepdims=True)
+    assert np.max(np.abs(G[sel] - Gr) / gscale) <= 1e-6

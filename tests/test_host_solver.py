@@ -103,6 +103,12 @@ def test_status_bits():
     assert out["status"][0] == 0 and out["status"][5] == 0
     assert all(out["status"][i] & nat.MTG_TRAJ_BAD_TIME for i in (1, 2, 3))
     assert out["status"][4] & nat.MTG_TRAJ_NOT_SPD
+    # 0 < T < DBL_EPSILON is a valid time for the reference's CHECK (lin_impl:287) but its A(T) is
+    # singular there (baseCoeffsWithTime keeps only the t = 0 entry, polynomial.h:225): NOT_SPD
+    t2 = times[:1].copy()
+    t2[0, 4] = 1e-17
+    tiny = mtg.host_solve_linear_batch(10, 4, vals[:1], mask[:1], t2, status=True)["status"][0]
+    assert tiny & nat.MTG_TRAJ_NOT_SPD and not tiny & nat.MTG_TRAJ_BAD_TIME, tiny
     # orders > N/2-1 are dropped with a warning (lin_impl:74-95): same result as without them
     v8, m8, t8 = mtg.random_vertices_path_batch(8, 3, 6, 8)
     a = mtg.host_solve_linear_batch(8, 3, v8, m8, t8, status=True)
