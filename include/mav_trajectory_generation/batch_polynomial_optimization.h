@@ -6,6 +6,11 @@
 // Arrays are in the C ABI layout (include/mtg.h): values [B][K+1][N/2][D], mask [B][K+1] (bit k:
 // derivative k fixed), times [B][K], coeffs [B][K][D][N].  Pass MTG_FLAG_DEVICE_PTRS to hand over
 // device pointers (inputs already in HBM); host pointers are staged by the library.
+//
+// Several devices: construct with a device list (e.g. allDevices()).  A host-array solve() is then
+// one mtg_solve_linear_batch_multi call: contiguous shards of the batch, one host thread and one
+// context per device, no collective; bit-identical to a one-device solve.  Device-
+// pointer calls and the other entry points run on the first device.
 #ifndef MAV_TRAJECTORY_GENERATION_BATCH_POLYNOMIAL_OPTIMIZATION_H_
 #define MAV_TRAJECTORY_GENERATION_BATCH_POLYNOMIAL_OPTIMIZATION_H_
 
@@ -48,10 +53,34 @@ class BatchPolynomialOptimization {
  public:
   enum { N = _N };
   BatchPolynomialOptimization(int dimension, int segments, int derivative_to_optimize, int device = 0)
+      : BatchPolynomialOptimization(dimension, segments, derivative_to_optimize, std::vector<int>{device}) {}
+  BatchPolynomialOptimization(int dimension, int segments, int derivative_to_optimize, const std::vector<int>& devices)
       : D_(dimension), K_(segments), r_(derivative_to_optimize) {
-    check(mtg_create(device, &ctx_), nullptr, "mtg_create");
+    if (devices.empty()) fail(MTG_ERR_INVALID_ARGUMENT, "BatchPolynomialOptimization: no device");
+    for (int device : devices) {
+      mtg_ctx* c = nullptr;
+      const int rc = mtg_create(device, &c);
+      if (rc != MTG_OK) {
+        for (mtg_ctx* o : ctxs_) mtg_destroy(o);
+        ctxs_.clear();
+        check(rc, nullptr, "mtg_create");
+      }
+      ctxs_.push_back(c);
+    }
+    ctx_ = ctxs_.front();
   }
-  ~BatchPolynomialOptimization() { mtg_destroy(ctx_); }
+  ~BatchPolynomialOptimization() {
+    for (mtg_ctx* c : ctxs_) mtg_destroy(c);
+  }
+  // every visible device: 0 .. mtg_device_count() - 1
+  static std::vector<int> allDevices() {
+    int n = 0;
+    check(mtg_device_count(&n), nullptr, "mtg_device_count");
+    std::vector<int> d(n);
+    for (int i = 0; i < n; ++i) d[i] = i;
+    return d;
+  }
+  int numDevices() const { return (int)ctxs_.size(); }
   BatchPolynomialOptimization(const BatchPolynomialOptimization&) = delete;
   BatchPolynomialOptimization& operator=(const BatchPolynomialOptimization&) = delete;
 
@@ -64,6 +93,12 @@ class BatchPolynomialOptimization {
   void solve(int64_t batch, const double* values, const uint8_t* mask, const double* times, double* coeffs,
              double* cost = nullptr, int32_t* status = nullptr, unsigned flags = 0, double* free_out = nullptr,
              int32_t* n_free = nullptr) {
+    if (ctxs_.size() > 1 && !(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_ASYNC))) {
+      check(mtg_solve_linear_batch_multi(ctxs_.data(), (int)ctxs_.size(), N, D_, K_, r_, batch, values, mask, times,
+                                         coeffs, free_out, n_free, cost, status, flags),
+            ctx_, "mtg_solve_linear_batch_multi");
+      return;
+    }
     check(mtg_solve_linear_batch(ctx_, N, D_, K_, r_, batch, values, mask, times, coeffs, free_out, n_free, cost,
                                  status, flags),
           ctx_, "mtg_solve_linear_batch");
@@ -144,6 +179,7 @@ class BatchPolynomialOptimization {
 
  private:
   int D_, K_, r_;
+  std::vector<mtg_ctx*> ctxs_;
   mtg_ctx* ctx_ = nullptr;
 };
 

@@ -127,6 +127,27 @@ int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_
                            int32_t* n_free_out, double* cost_out, int32_t* status,
                            unsigned flags);
 
+/* Contiguous shard `shard` (0 <= shard < n_shards) of a batch of `batch` independent problems:
+ * [*begin, *end) = [g ceil(B/G), min(B, (g+1) ceil(B/G))).  The partition that
+ * mtg_solve_linear_batch_multi, bench.py's ranks and the Python layer use.  No device work. */
+int mtg_shard_range(int64_t batch, int n_shards, int shard, int64_t* begin, int64_t* end);
+
+/* mtg_solve_linear_batch over several contexts, normally one per device (mtg_create(g, ...)), in one
+ * call: the batch is cut into n_ctxs contiguous shards (mtg_shard_range) and shard g is solved by
+ * ctxs[g] on its own host thread (the calling thread takes shard 0), each with its own staging /
+ * chunk pipeline, writing its disjoint slice of the outputs.  Trajectories are independent, so there
+ * is no collective.  This replaces a caller's loop of single solves over a whole batch
+ * (src/polynomial_timing_evaluation.cpp:119-126) with one call that uses every GPU of the node.
+ * Host arrays only (MTG_FLAG_DEVICE_PTRS and MTG_FLAG_ASYNC are rejected: device arrays live on one
+ * device); the call returns when every shard has landed.  Results are bit-identical to one
+ * mtg_solve_linear_batch over the whole batch.  On failure the first failing shard's code is
+ * returned and mtg_last_error(ctxs[0]) names the shard.  Distinct contexts run concurrently; a
+ * context listed twice serialises its shards. */
+int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D, int K, int derivative_to_optimize,
+                                 int64_t batch, const double* values, const uint8_t* fixed_mask,
+                                 const double* times, double* coeffs, double* free_out, int32_t* n_free_out,
+                                 double* cost_out, int32_t* status, unsigned flags);
+
 /* Batched Trajectory::evaluateRange (src/trajectory.cpp:68-128) over solved
  * trajectories, with the reference's sequential time accumulation (acc += dt)
  * reproduced exactly.  coeffs [B][K][D][N], times [B][K].  Sample counts are

@@ -57,6 +57,11 @@ _SIGNATURES = {
     "mtg_solve_linear_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp,
                                               _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_shard_range": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                       ctypes.POINTER(ctypes.c_int64)]),
+    "mtg_solve_linear_batch_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp,
+                                                    _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
     "mtg_evaluate_range_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int64, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double,
                                                 ctypes.c_double, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,

@@ -600,6 +600,64 @@ int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_
                    free_out, n_free_out, cost_out, status, 1, nullptr, flags);
 }
 
+int mtg_shard_range(int64_t batch, int n_shards, int shard, int64_t* begin, int64_t* end) {
+  if (batch < 0 || n_shards < 1 || shard < 0 || shard >= n_shards || !begin || !end) return MTG_ERR_INVALID_ARGUMENT;
+  const int64_t per = (batch + n_shards - 1) / n_shards;  // ceil(B / G), SURVEY.md 8(e)
+  *begin = std::min<int64_t>(batch, (int64_t)shard * per);
+  *end = std::min<int64_t>(batch, *begin + per);
+  return MTG_OK;
+}
+
+int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D, int K, int derivative_to_optimize,
+                                 int64_t batch, const double* values, const uint8_t* fixed_mask,
+                                 const double* times, double* coeffs, double* free_out, int32_t* n_free_out,
+                                 double* cost_out, int32_t* status, unsigned flags) {
+  if (!ctxs || n_ctxs < 1) return MTG_ERR_INVALID_ARGUMENT;
+  for (int g = 0; g < n_ctxs; ++g)
+    if (!ctxs[g]) return MTG_ERR_INVALID_ARGUMENT;
+  mtg_ctx* c0 = ctxs[0];
+  if (flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_ASYNC))
+    return set_error(c0, MTG_ERR_INVALID_ARGUMENT, "multi-device solves take host arrays and are synchronous");
+  int rc = check_shape(c0, N, D, K, derivative_to_optimize, batch);
+  if (rc != MTG_OK) return rc;
+  if (batch == 0) return MTG_OK;
+  if (!values || !fixed_mask || !times)
+    return set_error(c0, MTG_ERR_INVALID_ARGUMENT, "values, fixed_mask and times are required");
+  const int V = K + 1, h = N / 2;
+  const size_t s_vals = (size_t)V * h * D, s_coef = (size_t)K * D * N, s_free = (size_t)D * V * h;
+  std::vector<int> rcs(n_ctxs, MTG_OK);
+  auto shard = [&](int g) {
+    int64_t b0 = 0, b1 = 0;
+    mtg_shard_range(batch, n_ctxs, g, &b0, &b1);
+    if (b1 <= b0) return;
+    rcs[g] = mtg_solve_linear_batch(ctxs[g], N, D, K, derivative_to_optimize, b1 - b0, values + b0 * s_vals,
+                                    fixed_mask + b0 * V, times + b0 * K, coeffs ? coeffs + b0 * s_coef : nullptr,
+                                    free_out ? free_out + b0 * s_free : nullptr, n_free_out ? n_free_out + b0 : nullptr,
+                                    cost_out ? cost_out + b0 : nullptr, status ? status + b0 : nullptr, flags);
+  };
+  // one host thread per context: each drives its device's staging or chunk pipeline and writes its
+  // disjoint slice of the outputs (no collective); shard 0 runs on this thread
+  std::vector<std::thread> pool;
+  for (int g = 1; g < n_ctxs; ++g) {
+    try {
+      pool.emplace_back(shard, g);
+    } catch (...) {  // no thread: solve this shard here instead
+      shard(g);
+    }
+  }
+  shard(0);
+  for (auto& t : pool) t.join();
+  for (int g = 0; g < n_ctxs; ++g) {
+    if (rcs[g] == MTG_OK) continue;
+    if (g > 0) {
+      std::lock_guard<std::mutex> l(c0->mu);
+      c0->last_error = "shard " + std::to_string(g) + ": " + ctxs[g]->last_error;
+    }
+    return rcs[g];
+  }
+  return MTG_OK;
+}
+
 int mtg_time_sweep_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_optimize,
                          int64_t batch, const double* values, const uint8_t* fixed_mask,
                          const double* times, int n_candidates, const double* scales,

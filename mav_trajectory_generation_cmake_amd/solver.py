@@ -385,6 +385,43 @@ def solve_linear_batch(N, r, values, mask, times, device=0, **kw):
     return default_context(device).solve_linear_batch(N, r, values, mask, times, **kw)
 
 
+def shard_range(batch, n_shards, shard):
+    """[begin, end) of contiguous shard `shard` of `n_shards` (mtg_shard_range)."""
+    b, e = ctypes.c_int64(0), ctypes.c_int64(0)
+    nat.check(nat.load().mtg_shard_range(batch, n_shards, shard, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def solve_linear_batch_multi(contexts, N, r, values, mask, times, free=False, n_free=False, cost=False,
+                             status=False):
+    """One batch over several contexts (normally one per device) in one call
+    (mtg_solve_linear_batch_multi): contiguous shards, one host thread per context, host arrays in and
+    out; bit-identical to one Context.solve_linear_batch over the whole batch."""
+    lib = nat.load()
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    mask = np.ascontiguousarray(mask, dtype=np.uint8)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    B, V, h, D = values.shape
+    K = V - 1
+    assert h == N // 2 and mask.shape == (B, V) and times.shape == (B, K)
+    out = {"coeffs": np.empty((B, K, D, N))}
+    if free:
+        out["free"] = np.zeros((B, D, V * h))
+    if n_free:
+        out["n_free"] = np.empty((B,), np.int32)
+    if cost:
+        out["cost"] = np.empty((B,))
+    if status:
+        out["status"] = np.empty((B,), np.int32)
+    handles = (ctypes.c_void_p * len(contexts))(*[c.handle for c in contexts])
+    rc = lib.mtg_solve_linear_batch_multi(ctypes.cast(handles, ctypes.c_void_p), len(contexts), N, D, K, r, B,
+                                          _addr(values), _addr(mask), _addr(times), _addr(out["coeffs"]),
+                                          _addr(out.get("free")), _addr(out.get("n_free")), _addr(out.get("cost")),
+                                          _addr(out.get("status")), 0)
+    nat.check(rc, contexts[0].handle)
+    return out
+
+
 def host_solve_linear_batch(N, r, values, mask, times, free=False, n_free=False, cost=False, status=False,
                             threads=1):
     """The library's host (CPU) solve path (mtg_host_solve_linear_batch): same algorithm and outputs as

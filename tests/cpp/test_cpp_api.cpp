@@ -188,6 +188,15 @@ static void test_random_paths(int D, int K, int max_derivative, int r, int seeds
       // (computeCost forms Q with pow() the reference's way, lin_impl:574-589; the kernel's cost uses
       // the exact table: at N = 12 the two differ in the 8th digit)
       EXPECT(std::fabs(bcost[0] - cost) <= 1e-7 * std::fmax(cost, 1e-12), "batch cost %.17g vs %.17g", bcost[0], cost);
+      // several devices (here two contexts on device 0: the mtg_solve_linear_batch_multi path, one host
+      // thread per context): three copies of the problem, shards of 2 + 1, the same bits
+      BatchPolynomialOptimization<N> multi(D, K, r, std::vector<int>{0, 0});
+      EXPECT(multi.numDevices() == 2, "two contexts");
+      std::vector<double> mcoeffs;
+      multi.solve({vertices, vertices, vertices}, {times, times, times}, &mcoeffs);
+      const size_t per = (size_t)K * D * N;
+      for (size_t b = 0; b < 3; ++b)
+        for (size_t q = 0; q < per; ++q) EXPECT(mcoeffs[b * per + q] == coeffs[q], "multi-device batch vs one device");
     }
   }
 }

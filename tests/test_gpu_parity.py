@@ -730,3 +730,22 @@ def test_config5_full_size_vs_oracle(gpu_ctx):
     np.testing.assert_allclose(J[sel], Jr, rtol=1e-7, atol=0)
     gscale = np.max(np.abs(Gr), axis=2, keepdims=True)
     assert np.max(np.abs(G[sel] - Gr) / gscale) <= 1e-6
+
+
+@pytest.mark.parametrize("B,n_ctx", [(20001, 2), (5, 3), (2, 3)])
+def test_solve_linear_batch_multi_bitwise(gpu_ctx, B, n_ctx):
+    """mtg_solve_linear_batch_multi: contiguous shards over several contexts, one host thread each
+    (here all on device 0: the same code path as one context per device), bit-identical to one call
+    over the whole batch -- pipelined shards (20001: > 8 MB each), small staged shards, an empty shard."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    vals, mask, times = _bench_batch(B, seed0=9000)
+    ctxs = [gpu_ctx] + [mtg.Context(0) for _ in range(n_ctx - 1)]
+    try:
+        multi = mtg.solve_linear_batch_multi(ctxs, 10, 4, vals, mask, times, free=True, n_free=True, cost=True,
+                                             status=True)
+    finally:
+        for c in ctxs[1:]:
+            c.close()
+    one = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, free=True, n_free=True, cost=True, status=True)
+    for k in ("coeffs", "free", "n_free", "cost", "status"):
+        np.testing.assert_array_equal(multi[k], one[k], err_msg=k)

@@ -155,3 +155,24 @@ def test_segment_matrices():
     assert lib.mtg_host_segment_matrices(10, 4, 0.0, None, None, None, None) == nat.MTG_ERR_INVALID_ARGUMENT
     assert lib.mtg_host_segment_matrices(10, 5, 1.0, None, None, None, None) == nat.MTG_ERR_BAD_DERIVATIVE
     del ctypes
+
+
+def test_shard_range_partitions_the_batch():
+    """mtg_shard_range: shard g of G is [g ceil(B/G), min(B, (g+1) ceil(B/G))) -- contiguous, disjoint,
+    covering the batch; host solves of the shards concatenate bit-equal to one solve."""
+    for B in (0, 1, 7, 37, 1000, 125001):
+        for G in (1, 2, 3, 8):
+            ranges = [mtg.shard_range(B, G, g) for g in range(G)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == B
+            for (b0, b1), (c0, c1) in zip(ranges, ranges[1:]):
+                assert b1 == c0 and b0 <= b1
+            per = -(-B // G)
+            assert all(b1 - b0 <= per for b0, b1 in ranges)
+    with pytest.raises(nat.MTGError):
+        mtg.shard_range(10, 2, 2)
+    vals, mask, times = mtg.random_vertices_path_batch(10, 3, 10, 29, seed0=5)
+    whole = mtg.host_solve_linear_batch(10, 4, vals, mask, times, free=True, cost=True, status=True)
+    parts = [mtg.host_solve_linear_batch(10, 4, vals[b0:b1], mask[b0:b1], times[b0:b1], free=True, cost=True,
+                                         status=True) for b0, b1 in (mtg.shard_range(29, 3, g) for g in range(3))]
+    for k in ("coeffs", "free", "cost", "status"):
+        np.testing.assert_array_equal(np.concatenate([p[k] for p in parts]), whole[k])
