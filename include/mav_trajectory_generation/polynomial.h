@@ -6,7 +6,7 @@
 //
 // Not provided: computeRoots / computeMinMax* / selectMinMax* (Jenkins-Traub root finding,
 // src/rpoly.cpp, outside the ported path): extrema of whole trajectories go through
-// Trajectory::computeMinMaxMagnitude, which the library computes on the GPU.
+// Trajectory::computeMinMaxMagnitude (host or GPU, ExecutionPolicy).
 #ifndef MAV_TRAJECTORY_GENERATION_POLYNOMIAL_H_
 #define MAV_TRAJECTORY_GENERATION_POLYNOMIAL_H_
 

@@ -2,7 +2,7 @@
 // src/segment.cpp:27-58).
 //
 // Not provided: computeMinMaxMagnitudeCandidate{Times,s} / selectMinMaxMagnitudeFromCandidates
-// (root finding, src/rpoly.cpp); use Trajectory::computeMinMaxMagnitude (GPU).
+// (root finding, src/rpoly.cpp); use Trajectory::computeMinMaxMagnitude (host or GPU, ExecutionPolicy).
 #ifndef MAV_TRAJECTORY_GENERATION_SEGMENT_H_
 #define MAV_TRAJECTORY_GENERATION_SEGMENT_H_
 

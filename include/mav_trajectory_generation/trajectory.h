@@ -5,8 +5,8 @@
 // segment switch, sampling times restarting at the start segment's beginning), so its samples are
 // bit-identical to the reference's.  A single trajectory is sampled on the calling thread (the
 // library's GPU evaluateRange, mtg_evaluate_range_batch, is the batched form and gives the same
-// bits); under ExecutionPolicy::kDevice it goes through the GPU.  computeMinMaxMagnitude runs on
-// the GPU (mtg_min_max_magnitude_batch).
+// bits); under ExecutionPolicy::kDevice it goes through the GPU.  computeMinMaxMagnitude follows the
+// same policy (host: mtg_host_min_max_magnitude_batch; device: mtg_min_max_magnitude_batch).
 #ifndef MAV_TRAJECTORY_GENERATION_TRAJECTORY_H_
 #define MAV_TRAJECTORY_GENERATION_TRAJECTORY_H_
 
@@ -182,8 +182,9 @@ class Trajectory {
     if (sampling_times) sampling_times->assign(st.begin(), st.begin() + count);
   }
 
-  // src/trajectory.cpp:185-218 on the GPU (mtg_min_max_magnitude_batch): per segment the candidates
-  // t = 0, t = T and the real roots in [0, T] of the magnitude's derivative; segment-local times.
+  // src/trajectory.cpp:185-218: per segment the candidates t = 0, t = T and the real roots in [0, T]
+  // of the magnitude's derivative; segment-local times.  On the host (mtg_host_min_max_magnitude_batch)
+  // unless ExecutionPolicy::kDevice, which runs the GPU kernel (mtg_min_max_magnitude_batch).
   bool computeMinMaxMagnitude(int derivative, const std::vector<int>& dimensions, Extremum* minimum,
                               Extremum* maximum) const {
     check_notnull(minimum, "minimum");
@@ -198,11 +199,17 @@ class Trajectory {
     }
     std::vector<double> coeffs, times;
     pack(&coeffs, &times);
-    mtg_ctx* ctx = defaultContext();
     mtg_extremum mn, mx;
-    check(mtg_min_max_magnitude_batch(ctx, N_, D_, K(), 1, coeffs.data(), times.data(), derivative, mask, &mn, &mx,
-                                      0),
-          ctx, "mtg_min_max_magnitude_batch");
+    if (singleOnDevice()) {
+      mtg_ctx* ctx = defaultContext();
+      check(mtg_min_max_magnitude_batch(ctx, N_, D_, K(), 1, coeffs.data(), times.data(), derivative, mask, &mn, &mx,
+                                        0),
+            ctx, "mtg_min_max_magnitude_batch");
+    } else {  // the reference computes this on the CPU too
+      check(mtg_host_min_max_magnitude_batch(N_, D_, K(), 1, coeffs.data(), times.data(), derivative, mask, &mn, &mx,
+                                             1),
+            nullptr, "mtg_host_min_max_magnitude_batch");
+    }
     *minimum = Extremum(mn.time, mn.value, mn.segment);
     *maximum = Extremum(mx.time, mx.value, mx.segment);
     return true;

@@ -265,6 +265,15 @@ int mtg_host_solve_linear_batch(int N, int D, int K, int derivative_to_optimize,
                                 double* coeffs, double* free_out, int32_t* n_free_out, double* cost_out,
                                 int32_t* status, int threads);
 
+/* Host (CPU) path of mtg_min_max_magnitude_batch, no context and no GPU needed: the same candidates,
+ * root isolation and tie rules as the HIP kernel, on the calling thread(s).  The reference computes
+ * Trajectory::computeMinMaxMagnitude on the CPU (src/trajectory.cpp:181-218); the C++ drop-in uses
+ * this for its single trajectories unless ExecutionPolicy::kDevice.  All host pointers; threads <= 0:
+ * one per hardware thread. */
+int mtg_host_min_max_magnitude_batch(int N, int D, int K, int64_t batch, const double* coeffs, const double* times,
+                                     int derivative, uint32_t dimension_mask, mtg_extremum* minimum,
+                                     mtg_extremum* maximum, int threads);
+
 /* ---- Host utilities (no GPU): the reference's synthetic-input generators,
  * bit-exact with libstdc++ <random>, packed straight into the ABI layout.
  * Trajectory b of a batch uses seed (seed0 + b).  values [B][V][h][D],

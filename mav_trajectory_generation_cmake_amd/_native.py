@@ -89,6 +89,9 @@ _SIGNATURES = {
     "mtg_host_solve_linear_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                    ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
                                                    _c_dp, _c_dp, ctypes.c_int]),
+    "mtg_host_min_max_magnitude_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                                        _c_dp, _c_dp, ctypes.c_int, ctypes.c_uint32, _c_dp, _c_dp,
+                                                        ctypes.c_int]),
     "mtg_host_estimate_segment_times": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_double,
                                                        ctypes.c_double, ctypes.c_double, _c_dp]),
     "mtg_host_segment_matrices": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_double, _c_dp, _c_dp,

@@ -422,6 +422,21 @@ def solve_linear_batch_multi(contexts, N, r, values, mask, times, free=False, n_
     return out
 
 
+def host_min_max_magnitude_batch(coeffs, times, derivative, dimensions=None, threads=1):
+    """The library's host path of Context.min_max_magnitude_batch (mtg_host_min_max_magnitude_batch):
+    Trajectory::computeMinMaxMagnitude on the CPU, as the reference computes it (src/trajectory.cpp:181-218)."""
+    lib = nat.load()
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+    times = np.ascontiguousarray(times, dtype=np.float64)
+    B, K, D, N = coeffs.shape
+    mask = 0 if dimensions is None else int(sum(1 << int(d) for d in dimensions))
+    mn = np.zeros(B, dtype=EXTREMUM_DTYPE)
+    mx = np.zeros(B, dtype=EXTREMUM_DTYPE)
+    nat.check(lib.mtg_host_min_max_magnitude_batch(N, D, K, B, _addr(coeffs), _addr(times), int(derivative), mask,
+                                                   _addr(mn), _addr(mx), threads))
+    return mn, mx
+
+
 def host_solve_linear_batch(N, r, values, mask, times, free=False, n_free=False, cost=False, status=False,
                             threads=1):
     """The library's host (CPU) solve path (mtg_host_solve_linear_batch): same algorithm and outputs as

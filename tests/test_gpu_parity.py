@@ -749,3 +749,24 @@ def test_solve_linear_batch_multi_bitwise(gpu_ctx, B, n_ctx):
     one = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, free=True, n_free=True, cost=True, status=True)
     for k in ("coeffs", "free", "n_free", "cost", "status"):
         np.testing.assert_array_equal(multi[k], one[k], err_msg=k)
+
+
+@pytest.mark.parametrize("K", [3, 10, 20, 50])
+def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
+    """The extrema kernel (16 / 8 / 4 / 1 lanes per segment for K = 3 / 10 / 20 / 50) and the host
+    path (mtg_host_min_max_magnitude_batch, sequential scan) pick the same candidates: same segment,
+    values within 1e-12 (the kernel's Horner steps may contract to FMA, the host's do not)."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    N, r, B = 10, 4, 3000 if K <= 10 else 600
+    vals, mask, times = _bench_batch(B, seed0=77, K=K)
+    coeffs = gpu_ctx.solve_linear_batch(N, r, vals, mask, times)["coeffs"]
+    for derivative, dims in ((0, None), (1, None), (2, [0, 2]), (1, [2])):
+        g = gpu_ctx.min_max_magnitude_batch(coeffs, times, derivative, dims)
+        h = mtg.host_min_max_magnitude_batch(coeffs, times, derivative, dims, threads=8)
+        for a, c in zip(g, h):
+            scale = np.maximum(np.abs(h[1]["value"]), 1e-300)
+            assert np.max(np.abs(a["value"] - c["value"]) / scale) <= 1e-12
+            same = a["segment"] == c["segment"]
+            assert np.mean(same) >= 0.999
+            # a different segment only where two candidates' values tie to rounding
+            assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-12 * scale[~same])

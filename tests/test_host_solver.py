@@ -176,3 +176,22 @@ def test_shard_range_partitions_the_batch():
                                          status=True) for b0, b1 in (mtg.shard_range(29, 3, g) for g in range(3))]
     for k in ("coeffs", "free", "cost", "status"):
         np.testing.assert_array_equal(np.concatenate([p[k] for p in parts]), whole[k])
+
+
+@pytest.mark.parametrize("derivative,dims", [(1, None), (2, None), (1, [1]), (3, [0, 2])])
+def test_host_min_max_magnitude_vs_oracle(derivative, dims):
+    """mtg_host_min_max_magnitude_batch (the drop-in's Trajectory::computeMinMaxMagnitude on the CPU)
+    against the oracle (src/trajectory.cpp:181-218; numpy companion-matrix roots with the reference's
+    |imag| <= eps filter)."""
+    from oracle import pyoracle as O
+    N, r, K, B = 10, 4, 10, 24
+    vals, mask, times = mtg.random_vertices_path_batch(N, 3, K, B, seed0=1200)
+    coeffs = mtg.host_solve_linear_batch(N, r, vals, mask, times)["coeffs"]
+    mn, mx = mtg.host_min_max_magnitude_batch(coeffs, times, derivative, dims, threads=2)
+    for b in range(B):
+        rmn, rmx = O.min_max_magnitude(N, coeffs[b], times[b], derivative, dims)
+        for got, ref in ((mx[b], rmx), (mn[b], rmn)):
+            scale = max(abs(rmx[1]), 1e-300)
+            assert abs(got["value"] - ref[1]) <= 1e-9 * scale, (b, got, ref)
+            if got["segment"] == ref[2]:
+                assert abs(got["time"] - ref[0]) <= 1e-6 * times[b, ref[2]] or abs(got["value"] - ref[1]) <= 1e-12 * scale
