@@ -163,6 +163,23 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
                              const int64_t* offsets, double* out, double* sample_times,
                              unsigned flags);
 
+/* Batched Trajectory::evaluateRange in ONE call (the samples' total is not known in advance):
+ * counts[B] (samples per trajectory), offsets[B] (exclusive prefix sum of counts, in samples),
+ * *total (the sum) and the samples out [total][D] (+ sample_times [total], nullable) -- all computed
+ * on the device with no host round trip between them (the clock kernel also counts and scans; the
+ * sample kernel adds the block offsets).  `capacity` is the number of sample rows out (and
+ * sample_times) can hold.  If *total exceeds it, no sample is written and the call returns
+ * MTG_ERR_TOO_LARGE after counts, offsets and *total are filled (retry with capacity = *total); with
+ * MTG_FLAG_DEVICE_PTRS | MTG_FLAG_ASYNC the caller checks *total itself.  A safe capacity per
+ * trajectory is min(t_end, sum T_i) / dt + 2 (samples are taken while the accumulated time is below
+ * t_end and inside the trajectory), summed over the batch, with a little slack for the rounding of
+ * the accumulated clock.  With MTG_FLAG_DEVICE_PTRS every array (and total) is a device pointer;
+ * otherwise all are host pointers (the call then reads the total back once to size its staging). */
+int mtg_evaluate_range_batch_full(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                  const double* times, double t_start, double t_end, double dt, int derivative,
+                                  int64_t* counts, int64_t* offsets, int64_t* total, double* out,
+                                  double* sample_times, int64_t capacity, unsigned flags);
+
 /* Batched segment-time sweep (the nonlinear time-allocation objective,
  * polynomial_optimization_nonlinear_impl.h:765-832 via updateSegmentTimes +
  * solveLinear + computeCost): for each trajectory b and candidate c the

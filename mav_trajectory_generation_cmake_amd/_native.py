@@ -66,6 +66,10 @@ _SIGNATURES = {
                                                 ctypes.c_int64, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double,
                                                 ctypes.c_double, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,
                                                 ctypes.c_uint]),
+    "mtg_evaluate_range_batch_full": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_int64, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double,
+                                                     ctypes.c_double, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
+                                                     ctypes.c_int64, ctypes.c_uint]),
     "mtg_time_sweep_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_int,
                                             _c_dp, _c_dp, _c_dp, ctypes.c_uint]),

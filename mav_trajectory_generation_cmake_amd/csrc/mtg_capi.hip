@@ -986,6 +986,118 @@ int mtg_evaluate_range_batch(mtg_ctx* ctx, int N, int D, int K, int64_t batch,
   return MTG_OK;
 }
 
+int mtg_evaluate_range_batch_full(mtg_ctx* ctx, int N, int D, int K, int64_t batch, const double* coeffs,
+                                  const double* times, double t_start, double t_end, double dt, int derivative,
+                                  int64_t* counts, int64_t* offsets, int64_t* total, double* out,
+                                  double* sample_times, int64_t capacity, unsigned flags) {
+  if (!ctx) return MTG_ERR_INVALID_ARGUMENT;
+  if (N < 2 || N > 12 || (N % 2)) return set_error(ctx, MTG_ERR_UNSUPPORTED_N, "N must be even and in [2, 12]");
+  if (K < 1 || D < 1 || batch < 0 || capacity < 0)
+    return set_error(ctx, MTG_ERR_SIZE_MISMATCH, "need K >= 1, D >= 1, batch >= 0, capacity >= 0");
+  if (!(dt > 0.0) || derivative < 0)
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "dt must be > 0 and derivative >= 0");
+  if (!coeffs || !times || !counts || !offsets || !total || (capacity > 0 && !out))
+    return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "coeffs, times, counts, offsets, total and out are required");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  MTG_HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const bool dev = flags & MTG_FLAG_DEVICE_PTRS;
+  if (batch == 0) {
+    if (dev) MTG_HIP_TRY(ctx, hipMemsetAsync(total, 0, sizeof(int64_t), ctx->stream));
+    else *total = 0;
+    return MTG_OK;
+  }
+  int cap = 0;
+  const size_t wsb = mtg::eval_full_workspace_bytes(K, batch, &cap);
+  MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(wsb, 256)));
+  int64_t* d_total_ws = reinterpret_cast<int64_t*>(static_cast<char*>(ctx->workspace) + wsb - sizeof(int64_t));
+  if (dev) {
+    // counts, offsets (in-block prefix, then final) and the total, then the samples: four kernels on
+    // the stream, no host round trip in between
+    MTG_HIP_TRY(ctx, time_begin(ctx, false));
+    MTG_HIP_TRY(ctx, mtg::launch_eval_runs_counts(K, batch, times, t_start, t_end, dt, counts, offsets,
+                                                  ctx->workspace, cap, total, ctx->stream));
+    MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative, counts,
+                                            offsets, out, sample_times, ctx->workspace, cap, ctx->stream, true,
+                                            offsets, capacity));
+    MTG_HIP_TRY(ctx, time_end(ctx));
+    if (flags & MTG_FLAG_ASYNC) return MTG_OK;
+    int64_t tot = 0;
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(&tot, total, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (tot > capacity) {
+      char buf[160];
+      snprintf(buf, sizeof(buf), "evaluateRange needs %lld samples, capacity is %lld",
+               (long long)tot, (long long)capacity);
+      return set_error(ctx, MTG_ERR_TOO_LARGE, buf);
+    }
+    return MTG_OK;
+  }
+  // host arrays: counts and offsets first (one 8-B read of the total sizes the staging), then the
+  // samples straight into staging sized to the total
+  const size_t b_coef = sizeof(double) * (size_t)batch * K * D * N, b_times = sizeof(double) * (size_t)batch * K,
+               b_cnt = sizeof(int64_t) * (size_t)batch;
+  size_t off = 0;
+  const size_t o_times = off; off = align_up(off + b_times);
+  const size_t o_coef = off; off = align_up(off + b_coef);
+  const size_t o_cnt = off; off = align_up(off + b_cnt);
+  const size_t o_offs = off; off = align_up(off + b_cnt);
+  const size_t in_end = off;
+  MTG_HIP_TRY(ctx, ensure(&ctx->staging, &ctx->staging_bytes, std::max<size_t>(in_end, 256)));
+  char* base = static_cast<char*>(ctx->staging);
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_times, times, b_times, hipMemcpyHostToDevice, ctx->stream));
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(base + o_coef, coeffs, b_coef, hipMemcpyHostToDevice, ctx->stream));
+  int64_t* d_cnt = reinterpret_cast<int64_t*>(base + o_cnt);
+  int64_t* d_offs = reinterpret_cast<int64_t*>(base + o_offs);
+  MTG_HIP_TRY(ctx, time_begin(ctx, false));
+  MTG_HIP_TRY(ctx, mtg::launch_eval_runs_counts(K, batch, reinterpret_cast<const double*>(base + o_times), t_start,
+                                                t_end, dt, d_cnt, d_offs, ctx->workspace, cap, d_total_ws,
+                                                ctx->stream));
+  int64_t tot = 0;
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(&tot, d_total_ws, sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  *total = tot;
+  const size_t b_out = sizeof(double) * (size_t)(tot <= capacity ? tot : 0) * D;
+  const size_t b_st = sample_times ? sizeof(double) * (size_t)(tot <= capacity ? tot : 0) : 0;
+  const size_t o_out = in_end, o_st = align_up(o_out + b_out), all_end = align_up(o_st + b_st);
+  if (all_end > ctx->staging_bytes) {  // grow, keeping the staged inputs and counts
+    void* grown = nullptr;
+    MTG_HIP_TRY(ctx, hipMalloc(&grown, all_end));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(grown, ctx->staging, in_end, hipMemcpyDeviceToDevice, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    MTG_HIP_TRY(ctx, hipFree(ctx->staging));
+    ctx->staging = grown;
+    ctx->staging_bytes = all_end;
+    base = static_cast<char*>(grown);
+    d_cnt = reinterpret_cast<int64_t*>(base + o_cnt);
+    d_offs = reinterpret_cast<int64_t*>(base + o_offs);
+  }
+  if (tot > capacity) {  // counts, final offsets and the total for the caller's retry; no samples
+    MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<const double*>(base + o_coef),
+                                            reinterpret_cast<const double*>(base + o_times), t_start, t_end, dt,
+                                            derivative, d_cnt, d_offs, nullptr, nullptr, ctx->workspace, cap,
+                                            ctx->stream, true, d_offs, 0));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(counts, d_cnt, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipMemcpyAsync(offsets, d_offs, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
+    MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    char buf[160];
+    snprintf(buf, sizeof(buf), "evaluateRange needs %lld samples, capacity is %lld", (long long)tot,
+             (long long)capacity);
+    return set_error(ctx, MTG_ERR_TOO_LARGE, buf);
+  }
+  MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, reinterpret_cast<const double*>(base + o_coef),
+                                          reinterpret_cast<const double*>(base + o_times), t_start, t_end, dt,
+                                          derivative, d_cnt, d_offs, reinterpret_cast<double*>(base + o_out),
+                                          sample_times ? reinterpret_cast<double*>(base + o_st) : nullptr,
+                                          ctx->workspace, cap, ctx->stream, true, d_offs, capacity));
+  MTG_HIP_TRY(ctx, time_end(ctx));
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(counts, d_cnt, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
+  MTG_HIP_TRY(ctx, hipMemcpyAsync(offsets, d_offs, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
+  if (b_out) MTG_HIP_TRY(ctx, hipMemcpyAsync(out, base + o_out, b_out, hipMemcpyDeviceToHost, ctx->stream));
+  if (b_st) MTG_HIP_TRY(ctx, hipMemcpyAsync(sample_times, base + o_st, b_st, hipMemcpyDeviceToHost, ctx->stream));
+  MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return MTG_OK;
+}
+
 int mtg_last_kernel_ms(mtg_ctx* ctx, float* ms) {
   if (!ms) return MTG_ERR_INVALID_ARGUMENT;
   int n = 0;

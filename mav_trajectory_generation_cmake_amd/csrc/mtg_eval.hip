@@ -234,10 +234,19 @@ struct RunHead {
 // is a serial chain per trajectory; run here, 64 trajectories share a wave's lanes, where the eval
 // kernel's lane 0 would run it alone while its wave waits.  (16 or 32 trajectories per wave, i.e.
 // 4x / 2x the waves, measured slower: count 0.155 -> 0.205 / 0.166 ms at 1e4, scripts/eval_ab_env.sh.)
-__global__ void eval_runs_kernel(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
-                                 int cap, RunHead* heads, RunRec* runs) {
+//
+// With `counts` (the one-call evaluateRange, mtg_evaluate_range_batch_full) the kernel also finishes
+// each clock to get the trajectory's sample count -- the count kernel's work, without running the
+// clock twice -- and, per 64-trajectory block (one wave), writes the exclusive prefix sum of the
+// counts inside the block to offs[b] and the block's total to bsum[block]: the first level of the
+// device-side offsets (eval_scan_kernel, then the eval kernel adds the block's offset).
+__global__ __launch_bounds__(64) void eval_runs_kernel(int K, int64_t B, const double* times, double t_start,
+                                                       double t_end, double dt, int cap, RunHead* heads, RunRec* runs,
+                                                       int64_t* counts, int64_t* offs, int64_t* bsum) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  if (b >= B && !counts) return;
+  int64_t cnt = 0;
+  if (b < B) {
   Clock ck;
   ck.init(times + b * K, K, t_start, t_end, dt);
   RunRec* rr = runs + b * (int64_t)cap;
@@ -268,6 +277,51 @@ __global__ void eval_runs_kernel(int K, int64_t B, const double* times, double t
   h.seg = ck.seg;
   h.done = ck.done;
   heads[b] = h;
+  if (counts) {
+    while (ck.next(&r)) {  // the rest of a clock longer than the table: counted only
+    }
+    cnt = ck.n;
+    counts[b] = cnt;
+  }
+  }
+  if (!counts) return;
+  // exclusive prefix of the wave's counts (lanes past B count 0) and the block total
+  const int lane = threadIdx.x;
+  int64_t incl = cnt;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const int64_t o = __shfl_up(incl, m, 64);
+    if (lane >= m) incl += o;
+  }
+  if (b < B) offs[b] = incl - cnt;
+  if (lane == 63) bsum[blockIdx.x] = incl;
+}
+
+// Second level of the offsets: one block scans the per-block totals in place (exclusive) and writes
+// the grand total.  nb = ceil(B / 64) entries; each thread takes a contiguous chunk.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void eval_scan_kernel(int64_t nb, int64_t* bsum, int64_t* total) {
+  __shared__ int64_t part[kScanThreads];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + kScanThreads - 1) / kScanThreads;
+  const int64_t i0 = (int64_t)t * per < nb ? (int64_t)t * per : nb, i1 = i0 + per < nb ? i0 + per : nb;
+  int64_t s = 0;
+  for (int64_t i = i0; i < i1; ++i) s += bsum[i];
+  part[t] = s;
+  __syncthreads();
+  for (int m = 1; m < kScanThreads; m <<= 1) {  // inclusive scan of the chunk sums
+    const int64_t o = t >= m ? part[t - m] : 0;
+    __syncthreads();
+    part[t] += o;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;  // exclusive prefix of this chunk
+  for (int64_t i = i0; i < i1; ++i) {
+    const int64_t v = bsum[i];
+    bsum[i] = run;
+    run += v;
+  }
+  if (t == kScanThreads - 1) *total = part[t];
 }
 
 // Runs per round of the LDS table (from the run table, or built by lane 0), consumed by the wave.
@@ -292,7 +346,9 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
                                                                   double* sample_times, int cap,
-                                                                  const RunHead* heads, const RunRec* runs) {
+                                                                  const RunHead* heads, const RunRec* runs,
+                                                                  const int64_t* boff, int64_t* offsets_out,
+                                                                  int64_t capacity) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
   // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
 #pragma clang fp contract(off)
@@ -300,7 +356,10 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   const int64_t n_total = counts[b];
-  if (n_total <= 0) return;
+  // offsets: given (offsets[b]), or device-side (the in-block prefix offsets[b] + the block's offset)
+  const int64_t base = boff ? offsets[b] + boff[b >> 6] : offsets[b];
+  if (boff && lane == 0) offsets_out[b] = base;
+  if (n_total <= 0 || base + n_total > capacity) return;  // (past the caller's capacity: nothing written)
   RunLds* rt = reinterpret_cast<RunLds*>(lds);
   double* cf = reinterpret_cast<double*>(rt + 1);  // [K][D][N]
   double* ob = cf + K * D * N;                     // [kEvalThreads][D] output block
@@ -310,7 +369,6 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
   // not depend on t: formed once per coefficient here, with the same rounding as the reference's
   // per-sample products
   for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = base_coeff(derivative, i % N) * cb[i];
-  const int64_t base = offsets[b];
   Clock ck;
   int64_t stored = 0, next_run = 0;  // runs in the HBM table, runs taken from it
   const RunRec* rr = runs ? runs + b * (int64_t)cap : nullptr;
@@ -554,19 +612,43 @@ size_t eval_workspace_bytes(int K, int64_t B, int* cap) {
   return (size_t)B * (sizeof(RunHead) + (size_t)c * sizeof(RunRec));
 }
 
+size_t eval_full_workspace_bytes(int K, int64_t B, int* cap) {
+  // the run table, then the per-block totals and the grand total
+  return eval_workspace_bytes(K, B, cap) + sizeof(int64_t) * (size_t)((B + 63) / 64 + 1);
+}
+
+hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
+                                   int64_t* counts, int64_t* offsets, void* ws, int cap, int64_t* total,
+                                   hipStream_t stream) {
+  if (B == 0) return hipSuccess;
+  RunHead* heads = static_cast<RunHead*>(ws);
+  RunRec* runs = reinterpret_cast<RunRec*>(heads + B);
+  int64_t* bsum = reinterpret_cast<int64_t*>(runs + (size_t)B * cap);
+  const int64_t nb = (B + 63) / 64;
+  launch_kernel(eval_runs_kernel, dim3((unsigned)nb), dim3(64), 0, stream, K, B, times, t_start, t_end, dt, cap,
+                heads, runs, counts, offsets, bsum);
+  hipLaunchKernelGGL(eval_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, nb, bsum, total);
+  return hipGetLastError();
+}
+
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs, const double* times,
                              double t_start, double t_end, double dt, int derivative, const int64_t* counts,
                              const int64_t* offsets, double* out, double* sample_times, void* ws, int cap,
-                             hipStream_t stream) {
+                             hipStream_t stream, bool runs_ready, int64_t* offsets_out, int64_t capacity) {
   if (B == 0) return hipSuccess;
   RunHead* heads = nullptr;
   RunRec* runs = nullptr;
+  const int64_t* boff = nullptr;
   if (ws && cap > 0) {
     heads = static_cast<RunHead*>(ws);
     runs = reinterpret_cast<RunRec*>(heads + B);
-    const int block = 64;
-    launch_kernel(eval_runs_kernel, dim3((unsigned)((B + block - 1) / block)), dim3(block), 0, stream, K, B, times,
-                  t_start, t_end, dt, cap, heads, runs);
+    if (runs_ready) {  // launch_eval_runs_counts filled the table, the in-block offsets and the block offsets
+      boff = reinterpret_cast<const int64_t*>(runs + (size_t)B * cap);
+    } else {
+      const int block = 64;
+      launch_kernel(eval_runs_kernel, dim3((unsigned)((B + block - 1) / block)), dim3(block), 0, stream, K, B, times,
+                    t_start, t_end, dt, cap, heads, runs, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
+    }
   }
   // D = 3 (every reference problem in 3-D) has its own kernels: the sample loop's dimensions unrolled
   const bool d3 = D == 3;
@@ -580,10 +662,12 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   do {                                                                                                             \
     if (d3)                                                                                                        \
       launch_kernel(eval_range_kernel<NN, DER, 3>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
-                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs);  \
+                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
+                    offsets_out, capacity);                                                                        \
     else                                                                                                           \
       launch_kernel(eval_range_kernel<NN, DER, 0>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
-                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs);  \
+                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
+                    offsets_out, capacity);                                                                        \
   } while (0)
 #define MTG_EVAL_CASE(NN)                 \
   case NN:                                \

@@ -97,9 +97,22 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
                              double t_end, double dt, int64_t* counts, hipStream_t stream);
 // run-table workspace of launch_eval_range (bytes; *cap = runs stored per trajectory)
 size_t eval_workspace_bytes(int K, int64_t B, int* cap);
+// Samples of every trajectory (one block each).  Without runs_ready the run table is built first
+// (eval_runs_kernel); with runs_ready, launch_eval_runs_counts already built it together with the
+// counts and the two-level offsets: offsets then holds the in-block prefix and the kernel writes the
+// final offsets to offsets_out.  A trajectory whose samples would end past `capacity` samples is
+// not written.
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs,
                              const double* times, double t_start, double t_end, double dt,
                              int derivative, const int64_t* counts, const int64_t* offsets, double* out,
-                             double* sample_times, void* ws, int cap, hipStream_t stream);
+                             double* sample_times, void* ws, int cap, hipStream_t stream, bool runs_ready = false,
+                             int64_t* offsets_out = nullptr, int64_t capacity = INT64_MAX);
+// The one-call evaluateRange's first two kernels: the run table plus counts[B] and the in-block
+// offsets (eval_runs_kernel), then the block offsets and the grand total (eval_scan_kernel); all
+// device-side, no host round trip.  Workspace: eval_full_workspace_bytes.
+size_t eval_full_workspace_bytes(int K, int64_t B, int* cap);
+hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
+                                   int64_t* counts, int64_t* offsets, void* ws, int cap, int64_t* total,
+                                   hipStream_t stream);
 
 }  // namespace mtg

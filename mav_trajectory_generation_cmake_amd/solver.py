@@ -356,6 +356,68 @@ class Context:
                                                      _addr(out), _addr(st), 0), self.handle)
         return out[:total], (st[:total] if want_times else None), counts, offsets
 
+    def evaluate_range_batch_full(self, coeffs, times, t_start, t_end, dt, derivative=0, want_times=True,
+                                  capacity=None, asynchronous=False):
+        """Trajectory::evaluateRange for the batch in one call (mtg_evaluate_range_batch_full): counts,
+        offsets and samples computed on the device without a host round trip.  numpy arrays or torch
+        CUDA tensors (then every output is a device tensor on torch's current stream).  capacity: rows
+        of the sample buffer (default: evaluate_range_capacity, a safe bound); the call is retried
+        once with the exact total if it was short.  Returns (samples [S][D], sample_times [S] or None,
+        counts [B], offsets [B]); with asynchronous=True (device tensors only) the full-capacity
+        buffers and the device total are returned instead of the trimmed views: (samples, times,
+        counts, offsets, total)."""
+        dev = _is_torch(coeffs) and coeffs.is_cuda
+        B, K, D, N = coeffs.shape
+        if capacity is None:
+            capacity = evaluate_range_capacity(times, t_start, t_end, dt)
+        for attempt in range(2):
+            if dev:
+                import torch
+                kw = dict(device=coeffs.device)
+                counts = torch.empty(B, dtype=torch.int64, **kw)
+                offsets = torch.empty(B, dtype=torch.int64, **kw)
+                total = torch.zeros(1, dtype=torch.int64, **kw)
+                out = torch.empty((max(capacity, 1), D), dtype=torch.float64, **kw)
+                st = torch.empty(max(capacity, 1), dtype=torch.float64, **kw) if want_times else None
+                flags = nat.MTG_FLAG_DEVICE_PTRS | (nat.MTG_FLAG_ASYNC if asynchronous else 0)
+                self.set_stream(torch.cuda.current_stream(coeffs.device).cuda_stream)
+            else:
+                coeffs = np.ascontiguousarray(coeffs, dtype=np.float64)
+                times = np.ascontiguousarray(times, dtype=np.float64)
+                counts = np.empty(B, dtype=np.int64)
+                offsets = np.empty(B, dtype=np.int64)
+                total = np.zeros(1, dtype=np.int64)
+                out = np.empty((max(capacity, 1), D))
+                st = np.empty(max(capacity, 1)) if want_times else None
+                flags = 0
+                self.reset_stream()
+            rc = self._lib.mtg_evaluate_range_batch_full(self.handle, N, D, K, B, _addr(coeffs), _addr(times),
+                                                         float(t_start), float(t_end), float(dt), int(derivative),
+                                                         _addr(counts), _addr(offsets), _addr(total), _addr(out),
+                                                         _addr(st), int(capacity), flags)
+            if dev and asynchronous:
+                nat.check(rc, self.handle)
+                return out, st, counts, offsets, total
+            if rc == nat.MTG_ERR_TOO_LARGE and attempt == 0:
+                capacity = int(total[0])
+                continue
+            nat.check(rc, self.handle)
+            break
+        n = int(total[0])
+        return out[:n], (st[:n] if want_times else None), counts, offsets
+
+
+def evaluate_range_capacity(times, t_start, t_end, dt):
+    """A safe sample capacity for evaluateRange over a batch (mtg_evaluate_range_batch_full): per
+    trajectory the clock samples while the accumulated time (>= 0) is below t_end and the sample is
+    inside the trajectory, so at most min(t_end, sum T) / dt + 2 samples; 1e-9 relative slack for the
+    rounding of the accumulated clock."""
+    if _is_torch(times):
+        times = times.detach().cpu().numpy()
+    span = np.minimum(np.asarray(times, dtype=np.float64).sum(axis=1), float(t_end))
+    n = np.floor(np.maximum(span, 0.0) / float(dt) * (1.0 + 1e-9)) + 3
+    return int(n.sum())
+
 
 def full_vertex_values(values, mask, free, N):
     """All derivatives of every vertex [B][V][h][D]: the fixed values where the mask says fixed,

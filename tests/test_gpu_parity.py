@@ -770,3 +770,41 @@ def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
             assert np.mean(same) >= 0.999
             # a different segment only where two candidates' values tie to rounding
             assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-12 * scale[~same])
+
+
+@pytest.mark.parametrize("B", [1, 130, 2000])
+def test_evaluate_range_full_one_call(gpu_ctx, B):
+    """mtg_evaluate_range_batch_full: counts, offsets (device-side two-level scan) and samples in one
+    call are bit-identical to the two-call API (count, host prefix sum, eval), from numpy and from
+    device tensors; a short capacity returns MTG_ERR_TOO_LARGE with the exact total and the wrapper's
+    retry succeeds; trajectories that start past their end have no samples."""
+    torch = pytest.importorskip("torch")
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd.solver import _addr
+    vals, mask, times = _bench_batch(B, seed0=31, K=10)
+    coeffs = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times)["coeffs"]
+    t0 = float(np.median(times.sum(axis=1)))  # about half the trajectories start past their end
+    for (ts, te, dt, der) in [(0.0, 1e9, 0.01, 0), (t0 * 0.4, t0 * 1.1, 0.037, 2)]:
+        ref = gpu_ctx.evaluate_range_batch(coeffs, times, ts, te, dt, der)
+        got = gpu_ctx.evaluate_range_batch_full(coeffs, times, ts, te, dt, der)
+        for a, b in zip(got, ref):
+            np.testing.assert_array_equal(a, b)
+        c_d, t_d = torch.from_numpy(coeffs).cuda(), torch.from_numpy(times).cuda()
+        dv = gpu_ctx.evaluate_range_batch_full(c_d, t_d, ts, te, dt, der)
+        torch.cuda.synchronize()
+        for a, b in zip(dv, ref):
+            np.testing.assert_array_equal(a.cpu().numpy(), b)
+        total = int(ref[2].sum())
+        if total > 1:  # short capacity: the error, then the exact-size retry
+            counts = np.empty(B, np.int64)
+            offs = np.empty(B, np.int64)
+            tot = np.zeros(1, np.int64)
+            out = np.empty((total - 1, 3))
+            rc = gpu_ctx._lib.mtg_evaluate_range_batch_full(gpu_ctx.handle, 10, 3, 10, B, _addr(coeffs),
+                                                            _addr(times), ts, te, dt, der, _addr(counts),
+                                                            _addr(offs), _addr(tot), _addr(out), None, total - 1, 0)
+            assert rc == nat.MTG_ERR_TOO_LARGE and int(tot[0]) == total
+            np.testing.assert_array_equal(counts, ref[2])
+            np.testing.assert_array_equal(offs, ref[3])
+            got = gpu_ctx.evaluate_range_batch_full(coeffs, times, ts, te, dt, der, capacity=total - 1)
+            np.testing.assert_array_equal(got[0], ref[0])
