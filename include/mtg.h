@@ -79,6 +79,11 @@ extern "C" {
                                           instructions per trajectory, but latency-bound at one wave
                                           per SIMD: DESIGN.md 3.2) */
 
+#define MTG_FLAG_IP_KERNEL 32u         /* the interior-waypoint lane kernel where it applies (N in {6, 8, 10, 12},
+                                          D <= 4, K in {4, 8, 10, 12}, r >= 1; waves whose masks are not
+                                          the reference generators' pattern run the column kernel inside
+                                          it): DESIGN.md 3.1b */
+
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
 #define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave
                                           (MTG_FLAG_LANE_KERNEL) */
@@ -86,6 +91,8 @@ extern "C" {
                                           per dimension, twisted (K <= 12, N = 12 up to K = 20) */
 #define MTG_KERNEL_GENERAL 3           /* general LDS-resident fused kernel (any K) */
 #define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
+#define MTG_KERNEL_IP 5                /* one lane per chain, interior-waypoint pattern, LDL^T factors kept
+                                          (MTG_FLAG_IP_KERNEL) */
 
 typedef struct mtg_ctx mtg_ctx;
 

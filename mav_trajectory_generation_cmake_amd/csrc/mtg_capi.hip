@@ -352,7 +352,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 && !scales &&
       (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes) {
     const int rc = run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out,
-                                       cost_out, status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL));
+                                       cost_out, status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL));
     if (rc != kPipelineUnavailable) return rc;
   }
   mtg::SolveArgs a{};
@@ -453,7 +453,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL)));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL)));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (pin) {
@@ -494,7 +494,7 @@ int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned f
   size_t lds;
   if (!mtg::solve_geometry(N, D, K, &lg, &lds, &tpb)) return MTG_ERR_TOO_LARGE;
   if (flags & MTG_FLAG_SPLIT_KERNELS) return MTG_KERNEL_SPLIT;
-  return mtg::solve_kernel(N, D, K, flags);
+  return mtg::solve_kernel(N, D, K, flags, derivative_to_optimize);
 }
 
 const char* mtg_status_string(int code) {

@@ -58,12 +58,16 @@ bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes,
 // the general LDS-resident kernel (mtg_kernels.hip); MTG_FLAG_LANE_KERNEL selects the
 // lane-per-chain kernel (mtg_solve_lane.hip) where lane_geometry allows it, MTG_FLAG_GENERAL_KERNEL
 // the general kernel.
-int solve_kernel(int N, int D, int K, unsigned flags);  // MTG_KERNEL_LANE / _COLUMN / _GENERAL
+int solve_kernel(int N, int D, int K, unsigned flags, int r = -1);  // MTG_KERNEL_*
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags = 0);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);
 hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
 bool lane_geometry(int N, int D, int K, size_t* lds_bytes);
 hipError_t launch_solve_lane(int N, const SolveArgs& a, hipStream_t stream);
+// lane kernel of the interior-waypoint pattern (mtg_solve_ip.hip): ends fix every derivative,
+// interior vertices exactly their position; other waves run the column kernel's block function
+bool ip_geometry(int N, int D, int K, int r);
+hipError_t launch_solve_ip(int N, const SolveArgs& a, hipStream_t stream);
 
 // Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
 // workspace, then the block-Cholesky solve + recovery.

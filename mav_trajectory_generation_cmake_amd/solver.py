@@ -87,7 +87,7 @@ class Context:
         return np.array(buf[:got.value], dtype=np.float64)
 
     def solve_call(self, N, r, values, mask, times, coeffs, free=None, n_free=None, cost=None, status=None,
-                   split=False, general=False, lane=False):
+                   split=False, general=False, lane=False, ip=False):
         """A zero-argument callable that launches one device-pointer solve asynchronously on the
         current stream with the arguments bound once (the bench's step; minimal host overhead)."""
         import torch
@@ -97,6 +97,7 @@ class Context:
         flags = nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC | (nat.MTG_FLAG_SPLIT_KERNELS if split else 0)
         flags |= nat.MTG_FLAG_GENERAL_KERNEL if general else 0
         flags |= nat.MTG_FLAG_LANE_KERNEL if lane else 0
+        flags |= nat.MTG_FLAG_IP_KERNEL if ip else 0
         fn = self._lib.mtg_solve_linear_batch
         args = (self.handle, N, D, K, r, B, _addr(values), _addr(mask), _addr(times), _addr(coeffs), _addr(free),
                 _addr(n_free), _addr(cost), _addr(status), flags)
@@ -146,7 +147,8 @@ class Context:
 
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
-                           cost=None, status=None, split=False, asynchronous=False, general=False, lane=False):
+                           cost=None, status=None, split=False, asynchronous=False, general=False, lane=False,
+                           ip=False):
         """Solve a batch; returns dict of outputs (allocates those not given).
 
         want-flags: pass arrays (or True to allocate) for free / n_free / cost / status."""
@@ -193,6 +195,8 @@ class Context:
             flags |= nat.MTG_FLAG_GENERAL_KERNEL
         if lane:
             flags |= nat.MTG_FLAG_LANE_KERNEL
+        if ip:
+            flags |= nat.MTG_FLAG_IP_KERNEL
         rc = self._lib.mtg_solve_linear_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                               _addr(times), _addr(coeffs), _addr(free), _addr(n_free),
                                               _addr(cost), _addr(status), flags)
@@ -200,7 +204,7 @@ class Context:
         return out
 
     def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
-                         asynchronous=False, split=False):
+                         asynchronous=False, split=False, ip=False):
         dev = _is_torch(values) and values.is_cuda
         B, V, h, D = values.shape
         K = V - 1
@@ -220,6 +224,8 @@ class Context:
             self.reset_stream()
         if split:
             flags |= nat.MTG_FLAG_SPLIT_KERNELS
+        if ip:
+            flags |= nat.MTG_FLAG_IP_KERNEL
         rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                             _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
         nat.check(rc, self.handle)
