@@ -4,9 +4,15 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <pthread.h>
+#include <sched.h>
+
+#include <cctype>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <string>
@@ -15,6 +21,60 @@
 
 #include "mtg.h"
 #include "mtg_internal.h"
+
+// A persistent host thread of a context that runs one job at a time for the caller (the pipelined
+// solve's D2H issuer): created on first use and kept, instead of a std::thread per call (~50-100 us of
+// thread creation per host-array solve), and bound to the CPUs of the GPU's NUMA node where the
+// process may run there (the pageable-copy staging and completion waits then stay node-local).
+struct CtxWorker {
+  std::thread th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool has_job = false, quit = false;
+  ~CtxWorker() {
+    if (!th.joinable()) return;
+    {
+      std::lock_guard<std::mutex> g(m);
+      quit = true;
+    }
+    cv.notify_all();
+    th.join();
+  }
+  // start the thread (once); false if no thread can be created
+  bool start(const cpu_set_t* affinity) {
+    if (th.joinable()) return true;
+    try {
+      th = std::thread([this] {
+        std::unique_lock<std::mutex> l(m);
+        for (;;) {
+          cv.wait(l, [this] { return has_job || quit; });
+          if (quit) return;
+          std::function<void()> j = std::move(job);
+          l.unlock();
+          j();
+          l.lock();
+          has_job = false;
+          cv.notify_all();
+        }
+      });
+    } catch (...) {
+      return false;
+    }
+    if (affinity) (void)pthread_setaffinity_np(th.native_handle(), sizeof(cpu_set_t), affinity);
+    return true;
+  }
+  void post(std::function<void()> j) {
+    std::lock_guard<std::mutex> g(m);
+    job = std::move(j);
+    has_job = true;
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> l(m);
+    cv.wait(l, [this] { return !has_job; });
+  }
+};
 
 struct mtg_ctx {
   int device = 0;
@@ -41,6 +101,7 @@ struct mtg_ctx {
     size_t dev_bytes = 0;
   } pipe[kPipeSlots];
   hipEvent_t pipe_start = nullptr;
+  CtxWorker d2h_worker;
 };
 
 namespace mtg {
@@ -183,6 +244,54 @@ void destroy_pipe(mtg_ctx* ctx) {
   ctx->pipe_start = nullptr;
 }
 
+// The CPUs of the device's NUMA node that this process may run on (sysfs: the PCI device's numa_node
+// and the node's cpulist), or nullptr when unknown, empty, or MTG_NO_NUMA_BIND is set.
+const cpu_set_t* gpu_node_cpus(int device) {
+  constexpr int kDevs = 64;
+  static std::mutex mu;
+  static cpu_set_t sets[kDevs];
+  static bool known[kDevs] = {};
+  if (device < 0 || device >= kDevs) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (known[device]) return CPU_COUNT(&sets[device]) ? &sets[device] : nullptr;
+  cpu_set_t& set = sets[device];
+  CPU_ZERO(&set);
+  char bus[64] = {0};
+  const char* off = getenv("MTG_NO_NUMA_BIND");
+  if (!(off && *off && *off != '0') && hipDeviceGetPCIBusId(bus, sizeof(bus), device) == hipSuccess) {
+    for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+    int node = -1;
+    if (FILE* f = fopen(path, "r")) {
+      if (fscanf(f, "%d", &node) != 1) node = -1;
+      fclose(f);
+    }
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (node >= 0 && sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+      snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+      if (FILE* f = fopen(path, "r")) {
+        int a = 0, b = 0;
+        char sep = 0;
+        while (fscanf(f, "%d", &a) == 1) {
+          b = a;
+          if (fscanf(f, "%c", &sep) == 1 && sep == '-') {
+            if (fscanf(f, "%d", &b) != 1) b = a;
+            if (fscanf(f, "%c", &sep) != 1) sep = 0;
+          }
+          for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+          if (sep != ',') break;
+        }
+        fclose(f);
+      }
+    }
+  }
+  known[device] = true;
+  return CPU_COUNT(&set) ? &set : nullptr;
+}
+
 // host-pointer solves above this size go through the chunked pipeline
 constexpr size_t kPipelineMinBytes = 8u << 20;
 // returned by run_solve_pipelined when it could not start its D2H thread (nothing was issued)
@@ -269,12 +378,9 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       cv.notify_all();
     }
   };
-  std::thread d2h;
-  try {
-    d2h = std::thread(d2h_body);
-  } catch (...) {  // no thread (std::system_error): nothing was issued, the caller stages instead
-    return kPipelineUnavailable;
-  }
+  if (!ctx->d2h_worker.start(gpu_node_cpus(ctx->device)))
+    return kPipelineUnavailable;  // no thread (std::system_error): nothing was issued, the caller stages
+  ctx->d2h_worker.post(d2h_body);
   {
     // the pipeline's whole span (every chunk's H2D, kernel and D2H) is this call's timed interval;
     // the slot streams start after whatever the caller queued on the context's stream
@@ -327,7 +433,7 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
     launched = c + 1;
     cv.notify_all();
   }
-  d2h.join();
+  ctx->d2h_worker.wait();
   for (auto& s : ctx->pipe) (void)hipStreamSynchronize(s.stream);  // nothing may still read the caller's arrays
   if (err != hipSuccess) return set_hip_error(ctx, err, err_what);
   // close the timed interval after the last D2H of every slot
