@@ -1,6 +1,6 @@
 // Host-only ASan/UBSan driver (tests/test_sanitizers.py): the library's host code
 // (csrc/mtg_host.cpp: generators, segment-time estimate; csrc/mtg_host_solve.cpp: the host solve
-// path and the host matrices) and the oracle's C restatement, compiled with -fsanitize and run on
+// path and the host matrices; csrc/mtg_host_extrema.cpp: the host min/max magnitude) and the oracle's C restatement, compiled with -fsanitize and run on
 // small problems of every N, odd and even K, mixed masks, K = 1, and the rejected shapes.  Any
 // sanitizer report aborts the run (halt_on_error); the exit code is the number of failed checks.
 #include <cmath>
@@ -63,6 +63,15 @@ static void solve_case(int N, int D, int K, int r, int B, unsigned seed, bool mi
   CHECK(mtg_host_coefficients_from_vertices_batch(N, D, K, B, full.data(), times.data(), c2.data(), 2) == MTG_OK);
   std::vector<double> A(N * N), Ai(N * N), Q(N * N), H(N * N);
   CHECK(mtg_host_segment_matrices(N, r, times[0], A.data(), Ai.data(), Q.data(), H.data()) == MTG_OK);
+  // min / max magnitude of every derivative the host path accepts, all and one dimension
+  std::vector<mtg_extremum> mn(B), mx(B);
+  for (int k = 0; k <= N - 2; ++k) {
+    CHECK(mtg_host_min_max_magnitude_batch(N, D, K, B, coeffs.data(), times.data(), k, 0, mn.data(), mx.data(), 2) ==
+          MTG_OK);
+    CHECK(mtg_host_min_max_magnitude_batch(N, D, K, B, coeffs.data(), times.data(), k, 1u, mn.data(), nullptr, 1) ==
+          MTG_OK);
+    for (int b = 0; b < B; ++b) CHECK(mx[b].segment >= 0 && mx[b].segment < K && std::isfinite(mx[b].value));
+  }
   std::vector<double> oA(N * N), oAi(N * N), oQ(N * N);
   oracle_setup_mapping_matrix(N, times[0], oA.data());
   oracle_invert_mapping_matrix(N, oA.data(), oAi.data());

@@ -1,5 +1,5 @@
 """ASan/UBSan on the host code: the library's host sources (csrc/mtg_host.cpp,
-csrc/mtg_host_solve.cpp) and the oracle restatement (oracle/mtg_oracle.c), compiled with
+csrc/mtg_host_solve.cpp, csrc/mtg_host_extrema.cpp) and the oracle restatement (oracle/mtg_oracle.c), compiled with
 -fsanitize=address,undefined and driven by tests/sanitize/sanitize_driver.cpp.  Host code only: GPU
 sanitizers are not available on this pool.  The oracle is test infrastructure; it is compiled here
 as the checker the driver compares against."""
@@ -25,7 +25,8 @@ def test_host_code_under_asan_ubsan(tmp_path):
     exe = tmp_path / "sanitize_driver"
     subprocess.check_call(["g++", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
                            os.path.join(ROOT, "tests", "sanitize", "sanitize_driver.cpp"),
-                           os.path.join(CSRC, "mtg_host.cpp"), os.path.join(CSRC, "mtg_host_solve.cpp"), str(oracle_o),
+                           os.path.join(CSRC, "mtg_host.cpp"), os.path.join(CSRC, "mtg_host_solve.cpp"),
+                           os.path.join(CSRC, "mtg_host_extrema.cpp"), str(oracle_o),
                            "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-I", os.path.join(ROOT, "oracle"),
                            "-lpthread", "-lm"] + SAN)
     r = subprocess.run([str(exe)], env=env, capture_output=True, text=True, timeout=600)
