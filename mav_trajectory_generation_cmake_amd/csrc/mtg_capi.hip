@@ -92,14 +92,18 @@ struct mtg_ctx {
   std::string last_error;
   std::mutex mu;
   // Pipelined host-pointer solves (run_solve_pipelined): kPipeSlots chunks in flight, each with its
-  // own stream (H2D -> kernel -> D2H) and device buffers.
+  // own kernel stream and device buffers; all H2D copies go through one stream and all D2H copies
+  // through another (one copy queue per direction).
   static constexpr int kPipeSlots = 4;
   struct PipeSlot {
-    hipStream_t stream = nullptr;
-    hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;  // the chunk's kernel
+    hipEvent_t in_done = nullptr;  // its H2D copies landed (recorded on pipe_h2d)
+    hipEvent_t k_done = nullptr;   // its kernel finished (recorded on stream)
+    hipEvent_t done = nullptr;     // its D2H copies landed (recorded on pipe_d2h)
     void* dev = nullptr;  // device inputs + outputs of one chunk
     size_t dev_bytes = 0;
   } pipe[kPipeSlots];
+  hipStream_t pipe_h2d = nullptr, pipe_d2h = nullptr;
   hipEvent_t pipe_start = nullptr;
   CtxWorker d2h_worker;
 };
@@ -226,19 +230,32 @@ hipError_t ensure_pipe(mtg_ctx* ctx) {
   if (ctx->pipe_start) return hipSuccess;
   for (auto& s : ctx->pipe) {
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.k_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
     if (e != hipSuccess) return e;
   }
+  hipError_t e = hipStreamCreateWithFlags(&ctx->pipe_h2d, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->pipe_d2h, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
   return hipEventCreateWithFlags(&ctx->pipe_start, hipEventDisableTiming);
 }
 
 void destroy_pipe(mtg_ctx* ctx) {
+  for (hipStream_t* q : {&ctx->pipe_h2d, &ctx->pipe_d2h}) {
+    if (*q) (void)hipStreamSynchronize(*q);
+  }
   for (auto& s : ctx->pipe) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.dev) (void)hipFree(s.dev);
-    if (s.done) (void)hipEventDestroy(s.done);
+    for (hipEvent_t ev : {s.in_done, s.k_done, s.done})
+      if (ev) (void)hipEventDestroy(ev);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = mtg_ctx::PipeSlot{};
+  }
+  for (hipStream_t* q : {&ctx->pipe_h2d, &ctx->pipe_d2h}) {
+    if (*q) (void)hipStreamDestroy(*q);
+    *q = nullptr;
   }
   if (ctx->pipe_start) (void)hipEventDestroy(ctx->pipe_start);
   ctx->pipe_start = nullptr;
@@ -299,12 +316,16 @@ constexpr int kPipelineUnavailable = 1;
 
 // Host-pointer batch solve as a pipeline of chunks (the reference's equivalent is a
 // loop of single solves, src/polynomial_timing_evaluation.cpp:119-126).  Each of kPipeSlots slots
-// has its own stream and device buffers.  This thread issues, per chunk, the H2D copies and the
-// kernel; a second host thread issues the chunk's D2H copies and retires it.  So the H2D of chunk
-// c+1 runs on one DMA direction while the D2H of chunk c runs on the other (PCIe is full duplex:
-// ~57 GB/s each way on MI355X, 97 GB/s both, scripts/pcie_bw.py), whether the caller's arrays are
-// pinned (asynchronous copies) or pageable (the runtime's own staging, which blocks the issuing
-// thread -- hence two threads).  A slot is reused only after its previous chunk's D2H completed.
+// has its own kernel stream and device buffers.  This thread issues, per chunk, the H2D copies (on
+// the context's one H2D stream) and the kernel (on the slot's stream, after the copies); a second
+// host thread issues the chunk's D2H copies (on the one D2H stream, after the kernel) and retires
+// it.  So the H2D of chunk c+1 runs on one DMA direction while the D2H of chunk c runs on the other
+// (PCIe is full duplex: ~57 GB/s each way on MI355X, 97 GB/s both, scripts/pcie_bw.py), whether the
+// caller's arrays are pinned (asynchronous copies) or pageable (the runtime's own staging, which
+// blocks the issuing thread -- hence two threads).  One stream per copy direction: with the copies
+// on the four slot streams, a pinned caller's copies of both directions were spread over the
+// runtime's copy queues and the call ran in two modes (config 2, B = 125000: 7.0 or ~10-13 ms per
+// call, median 9.8; pageable 6.6 ms).  A slot is reused only after its previous chunk's D2H completed.
 int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const double* values,
                         const uint8_t* mask, const double* times, double* coeffs, double* free_out,
                         int32_t* n_free_out, double* cost_out, int32_t* status, unsigned kflags) {
@@ -359,15 +380,16 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       const int64_t b0 = c * chunk, nb = std::min<int64_t>(chunk, batch - b0);
       const char* dp = static_cast<const char*>(s.dev);
       auto copy = [&](void* user, size_t o, size_t sz) -> hipError_t {
-        return sz ? hipMemcpyAsync((char*)user + b0 * sz, dp + o, nb * sz, hipMemcpyDeviceToHost, s.stream)
+        return sz ? hipMemcpyAsync((char*)user + b0 * sz, dp + o, nb * sz, hipMemcpyDeviceToHost, ctx->pipe_d2h)
                   : hipSuccess;
       };
-      e = copy(coeffs, o_coef, s_coef);
+      e = hipStreamWaitEvent(ctx->pipe_d2h, s.k_done, 0);
+      if (e == hipSuccess) e = copy(coeffs, o_coef, s_coef);
       if (e == hipSuccess) e = copy(free_out, o_free, s_free);
       if (e == hipSuccess) e = copy(n_free_out, o_nfree, s_nfree);
       if (e == hipSuccess) e = copy(cost_out, o_cost, s_cost);
       if (e == hipSuccess) e = copy(status, o_status, s_status);
-      if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+      if (e == hipSuccess) e = hipEventRecord(s.done, ctx->pipe_d2h);
       // retire the previous chunk (its copies queued before this one's, so the DMA engine never
       // idles between chunks while this thread waits), and the last one at the end
       if (e == hipSuccess && c > 0) e = hipEventSynchronize(ctx->pipe[(c - 1) % S].done);
@@ -386,8 +408,7 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
     // the slot streams start after whatever the caller queued on the context's stream
     hipError_t e = time_begin(ctx, false);
     if (e == hipSuccess) e = hipEventRecord(ctx->pipe_start, ctx->stream);
-    for (auto& s : ctx->pipe)
-      if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, ctx->pipe_start, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->pipe_h2d, ctx->pipe_start, 0);
     if (e != hipSuccess) fail(e, "pipeline start");
   }
   // H2D + kernel issuer (this thread)
@@ -400,13 +421,15 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
     mtg_ctx::PipeSlot& s = ctx->pipe[c % S];
     const int64_t b0 = c * chunk, nb = std::min<int64_t>(chunk, batch - b0);
     char* dp = static_cast<char*>(s.dev);
+    hipStream_t up = ctx->pipe_h2d;
     hipError_t e = hipMemcpyAsync(dp + o_vals, (const char*)values + b0 * s_vals, nb * s_vals,
-                                  hipMemcpyHostToDevice, s.stream);
+                                  hipMemcpyHostToDevice, up);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(dp + o_mask, (const char*)mask + b0 * s_mask, nb * s_mask, hipMemcpyHostToDevice, s.stream);
+      e = hipMemcpyAsync(dp + o_mask, (const char*)mask + b0 * s_mask, nb * s_mask, hipMemcpyHostToDevice, up);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(dp + o_times, (const char*)times + b0 * s_times, nb * s_times, hipMemcpyHostToDevice,
-                         s.stream);
+      e = hipMemcpyAsync(dp + o_times, (const char*)times + b0 * s_times, nb * s_times, hipMemcpyHostToDevice, up);
+    if (e == hipSuccess) e = hipEventRecord(s.in_done, up);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s.stream, s.in_done, 0);
     if (e == hipSuccess && free_out) e = hipMemsetAsync(dp + o_free, 0, nb * s_free, s.stream);
     if (e == hipSuccess) {
       mtg::SolveArgs a{};
@@ -425,6 +448,7 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       a.status = status ? reinterpret_cast<int32_t*>(dp + o_status) : nullptr;
       e = mtg::launch_solve(N, a, s.stream, kflags);
     }
+    if (e == hipSuccess) e = hipEventRecord(s.k_done, s.stream);
     if (e != hipSuccess) {
       fail(e, "pipelined H2D / launch");
       break;
@@ -434,13 +458,14 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
     cv.notify_all();
   }
   ctx->d2h_worker.wait();
-  for (auto& s : ctx->pipe) (void)hipStreamSynchronize(s.stream);  // nothing may still read the caller's arrays
+  // nothing may still read or write the caller's arrays
+  (void)hipStreamSynchronize(ctx->pipe_h2d);
+  for (auto& s : ctx->pipe) (void)hipStreamSynchronize(s.stream);
+  (void)hipStreamSynchronize(ctx->pipe_d2h);
   if (err != hipSuccess) return set_hip_error(ctx, err, err_what);
-  // close the timed interval after the last D2H of every slot
-  for (auto& s : ctx->pipe) {
-    MTG_HIP_TRY(ctx, hipEventRecord(s.done, s.stream));
-    MTG_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, s.done, 0));
-  }
+  // close the timed interval after the last D2H (every D2H is on pipe_d2h, in chunk order)
+  MTG_HIP_TRY(ctx, hipEventRecord(ctx->pipe[(n_chunks - 1) % S].done, ctx->pipe_d2h));
+  MTG_HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->pipe[(n_chunks - 1) % S].done, 0));
   MTG_HIP_TRY(ctx, time_end(ctx));
   MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   return MTG_OK;
