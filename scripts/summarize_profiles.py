@@ -51,7 +51,10 @@ def counter_means(path, skip_first=2):
         if seen[key] <= skip_first:
             continue
         per.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    out = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in per.items()}
+    for k in out:
+        out[k]["grid"] = grid[k]
+    return out
 
 
 def short(name):
@@ -78,6 +81,13 @@ def main():
                     pmc.setdefault(k, {}).update(d)
         summary = {"batch": int(B), "source": "rocprofv3 --kernel-trace --pmc, one pass per counter group "
                                               "(scripts/profile.sh)", "kernels": {}}
+        # per short kernel name, the instantiation with the largest grid is the bench's own launch
+        # (the end_to_end leg's chunks can run another instantiation of the same kernel)
+        best = {}
+        for k, d in pmc.items():
+            sk = short(k)
+            if sk not in best or d.get("grid", 0) > pmc[best[sk]].get("grid", 0):
+                best[sk] = k
         for k, d in pmc.items():
             ent = dict(d)
             if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
@@ -85,7 +95,7 @@ def main():
             if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
                 ent["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0)
             summary["kernels"][k] = ent
-            if "hbm_bytes_per_launch" in ent:
+            if "hbm_bytes_per_launch" in ent and best.get(short(k)) == k:
                 key = "%s|%s" % (short(k), os.environ.get("WORKLOAD", "config2"))
                 traffic.setdefault(key, {})[str(B)] = {
                     "hbm_bytes_per_launch": ent["hbm_bytes_per_launch"],
