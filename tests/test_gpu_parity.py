@@ -6,6 +6,8 @@ segment.  Against the 60-digit truth fixtures the GPU path must be within
 1e-9 (it measures ~1e-12, N=12/K=20 ~1e-11); against the FP64 oracle (the
 reference algorithm restated) within 1e-6 for N=10 (north_star's 1e-6).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -820,6 +822,28 @@ def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
             same = a["segment"] == c["segment"]
             assert np.mean(same) >= 0.999
             # a different segment only where two candidates' values tie to rounding
+            assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-11 * scale[~same])
+
+
+@pytest.mark.parametrize("N", [8, 12])
+def test_min_max_magnitude_many_dimensions(gpu_ctx, N):
+    """More selected dimensions than the kernel stages per pass (4): D = 6 runs two staging passes
+    for f and takes the magnitudes from global memory; masks of 6, 5 and 1 dimensions, against the
+    host path (mtg_host_min_max_magnitude_batch)."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    rng = np.random.default_rng(31)
+    B, K, D = 500, 7, 6
+    fact = np.array([math.factorial(j) for j in range(N)], dtype=np.float64)
+    coeffs = rng.standard_normal((B, K, D, N)) / fact
+    times = rng.uniform(0.5, 2.0, size=(B, K))
+    for derivative, dims in ((0, None), (1, [0, 1, 2, 4, 5]), (2, [3])):
+        g = gpu_ctx.min_max_magnitude_batch(coeffs, times, derivative, dims)
+        h = mtg.host_min_max_magnitude_batch(coeffs, times, derivative, dims, threads=8)
+        for a, c in zip(g, h):
+            scale = np.maximum(np.abs(h[1]["value"]), 1e-300)
+            assert np.max(np.abs(a["value"] - c["value"]) / scale) <= 1e-11
+            same = a["segment"] == c["segment"]
+            assert np.mean(same) >= 0.99
             assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-11 * scale[~same])
 
 
