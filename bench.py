@@ -241,7 +241,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; (more ranks than GPUs, as in a rehearsal of the multi-rank path on a smaller
+    # box, share them round-robin)
+    ndev = torch.cuda.device_count()
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
     if world > 1:
         # gloo: the ranks exchange only a barrier and one scalar (no data-path collective), so the
         # multi-GPU run does not depend on RCCL
