@@ -847,6 +847,28 @@ def test_min_max_magnitude_many_dimensions(gpu_ctx, N):
             assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-11 * scale[~same])
 
 
+@pytest.mark.parametrize("N,K,D,B,derivative", [(10, 256, 3, 7, 1), (12, 256, 4, 5, 0), (6, 1, 1, 1, 4),
+                                                  (8, 33, 2, 65, 6), (4, 64, 5, 300, 2), (2, 12, 3, 50, 0)])
+def test_min_max_magnitude_edge_shapes(gpu_ctx, N, K, D, B, derivative):
+    """Edge shapes of the extrema kernel against the host path: the largest K (256 segments: 2 lanes
+    per segment and the staging reduced to fit the block's LDS), one segment of one dimension, the
+    highest derivative (f of degree 1), K just above a lane-group boundary, and N = 2 / 4."""
+    import mav_trajectory_generation_cmake_amd as mtg
+    rng = np.random.default_rng(N * 1000 + K)
+    fact = np.array([math.factorial(j) for j in range(N)], dtype=np.float64)
+    coeffs = rng.standard_normal((B, K, D, N)) / fact
+    times = rng.uniform(0.2, 3.0, size=(B, K))
+    for dims in (None, [D - 1]):
+        g = gpu_ctx.min_max_magnitude_batch(coeffs, times, derivative, dims)
+        h = mtg.host_min_max_magnitude_batch(coeffs, times, derivative, dims, threads=4)
+        for a, c in zip(g, h):
+            scale = np.maximum(np.abs(h[1]["value"]), 1e-300)
+            assert np.max(np.abs(a["value"] - c["value"]) / scale) <= 1e-11
+            same = a["segment"] == c["segment"]
+            assert np.all(np.abs(a["value"][~same] - c["value"][~same]) <= 1e-11 * scale[~same])
+            assert np.all((a["segment"] >= 0) & (a["segment"] < K))
+
+
 @pytest.mark.parametrize("B", [1, 130, 2000])
 def test_evaluate_range_full_one_call(gpu_ctx, B):
     """mtg_evaluate_range_batch_full: counts, offsets (device-side two-level scan) and samples in one
