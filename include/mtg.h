@@ -84,6 +84,11 @@ extern "C" {
                                           the reference generators' pattern run the column kernel inside
                                           it): DESIGN.md 3.1b */
 
+#define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10, K = 10, D <= 4, r >= 1;
+                                          one lane per (chain, dimension), waves whose masks are not the
+                                          reference generators' pattern run the column kernel inside it):
+                                          DESIGN.md 3.2c */
+
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
 #define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave
                                           (MTG_FLAG_LANE_KERNEL) */
@@ -93,6 +98,8 @@ extern "C" {
 #define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
 #define MTG_KERNEL_IP 5                /* one lane per chain, interior-waypoint pattern, LDL^T factors kept
                                           (MTG_FLAG_IP_KERNEL) */
+#define MTG_KERNEL_DL 6                /* one lane per (chain, dimension), interior-waypoint pattern
+                                          (MTG_FLAG_DL_KERNEL) */
 
 typedef struct mtg_ctx mtg_ctx;
 

@@ -68,6 +68,9 @@ hipError_t launch_solve_lane(int N, const SolveArgs& a, hipStream_t stream);
 // interior vertices exactly their position; other waves run the column kernel's block function
 bool ip_geometry(int N, int D, int K, int r);
 hipError_t launch_solve_ip(int N, const SolveArgs& a, hipStream_t stream);
+// dimension-lane kernel of the same pattern (mtg_solve_dl.hip): one lane per (chain, dimension)
+bool dl_geometry(int N, int D, int K, int r);
+hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream);
 
 // Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
 // workspace, then the block-Cholesky solve + recovery.

@@ -413,6 +413,7 @@ int solve_kernel(int N, int D, int K, unsigned flags, int r) {
   if (flags & MTG_FLAG_GENERAL_KERNEL) return MTG_KERNEL_GENERAL;
   if ((flags & MTG_FLAG_LANE_KERNEL) && lane_geometry(N, D, K, &lds)) return MTG_KERNEL_LANE;
   if ((flags & MTG_FLAG_IP_KERNEL) && r >= 0 && ip_geometry(N, D, K, r)) return MTG_KERNEL_IP;
+  if ((flags & MTG_FLAG_DL_KERNEL) && r >= 0 && dl_geometry(N, D, K, r)) return MTG_KERNEL_DL;
   if (reg_geometry(N, D, K, &lg, &lds)) return MTG_KERNEL_COLUMN;
   return MTG_KERNEL_GENERAL;
 }
@@ -421,6 +422,7 @@ hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned 
   switch (solve_kernel(N, a.D, a.K, flags, a.r)) {
     case MTG_KERNEL_LANE: return launch_solve_lane(N, a, stream);
     case MTG_KERNEL_IP: return launch_solve_ip(N, a, stream);
+    case MTG_KERNEL_DL: return launch_solve_dl(N, a, stream);
     case MTG_KERNEL_COLUMN: return launch_solve_reg(N, a, stream);
     default: break;
   }

@@ -24,7 +24,7 @@ ORACLE_TOL_N10 = 1e-6
 # (MTG_FLAG_LANE_KERNEL, where it applies), the general LDS-resident fused kernel, and the two-kernel
 # split path
 PATHS = {"default": {}, "lane": {"lane": True}, "general": {"general": True}, "split": {"split": True},
-         "ip": {"ip": True}}
+         "ip": {"ip": True}, "dl": {"dl": True}}
 
 
 def _oracle():
@@ -220,7 +220,7 @@ def test_paths_agree_mixed_masks(gpu_ctx):
     for p, o in outs.items():
         assert np.all(o["status"] == 0), p
         assert scale_normalised_error(o["coeffs"], ref, times) <= 1e-6, p
-    for p in ("lane", "general", "split", "ip"):
+    for p in ("lane", "general", "split", "ip", "dl"):
         assert scale_normalised_error(outs[p]["coeffs"], outs["default"]["coeffs"], times) <= 1e-9, p
 
 
@@ -961,3 +961,83 @@ def test_ip_kernel_time_sweep_and_status(gpu_ctx):
     assert o["status"][4] & nat.MTG_TRAJ_NOT_SPD and not o["status"][4] & nat.MTG_TRAJ_BAD_TIME
     assert o["status"][5] & nat.MTG_TRAJ_NOT_SPD
     assert np.all(o["status"][6:] == 0) and np.all(o["status"][:3] == 0)
+
+
+@pytest.mark.parametrize("D,r", [(3, 4), (1, 4), (2, 3), (4, 4), (3, 3)])
+def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
+    """The dimension-lane kernel (MTG_FLAG_DL_KERNEL): the reference generators' pattern against the
+    IP kernel (same arithmetic per dimension; the compiler contracts products into FMAs differently in
+    the two kernels, which the conditioning of R_pp amplifies to ~3e-10: 1e-9), the column kernel
+    (1e-8, scale-normalised: the host path and the oracle differ by up to 1.4e-8 on these batches) and
+    the oracle; free values, n_free, cost and status; a ragged last wave; a wave whose masks break the
+    pattern runs the column kernel's block function inside it, bit-identical to it."""
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
+    O = _oracle()
+    N, K = 10, 10
+    assert nat.solve_kernel(N, D, K, r, nat.MTG_FLAG_DL_KERNEL) == "solve_dl_kernel"
+    tpw = 64 // (2 * D)
+    B = 7 * tpw + 3
+    vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=91, max_derivative=N // 2 - 1)
+    # (the generator's times for D != 3 include segments of a few hundredths of a second next to ones
+    # of ten seconds: R_pp is then so ill-conditioned that any two FP64 orderings differ at 1e-6 --
+    # the host path differs from the oracle by 1e-2 on one of them -- so the comparison keeps T >= 0.5)
+    times = np.maximum(times, 0.5)
+    kw = dict(status=True, cost=True, free=True, n_free=True)
+    dl = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, dl=True, **kw)
+    ip = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, ip=True, **kw)
+    col = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    assert np.all(dl["status"] == 0)
+    np.testing.assert_array_equal(dl["n_free"], col["n_free"])
+    assert scale_normalised_error(dl["coeffs"], ip["coeffs"], times) <= 1e-9
+    assert scale_normalised_error(dl["coeffs"], col["coeffs"], times) <= 1e-8
+    np.testing.assert_allclose(dl["cost"], col["cost"], rtol=1e-9)
+    fs = np.max(np.abs(col["free"]), axis=2, keepdims=True)
+    assert np.max(np.abs(dl["free"] - col["free"]) / fs) <= 1e-8
+    ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
+    assert scale_normalised_error(dl["coeffs"], ref, times) <= 1e-6
+    assert check_path(vals, mask, times, dl["coeffs"], N, relative=True) < 1e-6
+    # a wave with another pattern: trajectory 2 tpw + 1 fixes a velocity at vertex 2
+    m2 = mask.copy()
+    m2[2 * tpw + 1, 2] |= 2
+    dl2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, dl=True, **kw)
+    col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, **kw)
+    w = slice(2 * tpw, 3 * tpw)
+    for k in ("coeffs", "cost", "free", "status"):
+        np.testing.assert_array_equal(dl2[k][w], col2[k][w], err_msg=k)
+        np.testing.assert_array_equal(dl2[k][:2 * tpw], dl[k][:2 * tpw], err_msg=k)
+        np.testing.assert_array_equal(dl2[k][3 * tpw:], dl[k][3 * tpw:], err_msg=k)
+
+
+def test_dl_kernel_time_sweep_status_and_device_outputs(gpu_ctx):
+    """The DL kernel under the time sweep (trajectory x candidate pairs, scaled times) equals the
+    column kernel's sweep; bad and tiny segment times set the same status bits; coefficients only
+    (no optional outputs) and an 8-B-aligned output array give the same values."""
+    import torch
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    vals, mask, times = _bench_batch(70, seed0=5)
+    scales = np.array([0.7, 1.0, 1.9])
+    a = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, dl=True)
+    b = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales)
+    np.testing.assert_allclose(a, b, rtol=1e-9)
+    t = times.copy()
+    t[3, 2] = 0.0
+    t[4, 7] = 1e-17
+    t[5, :] = 1e200
+    o = gpu_ctx.solve_linear_batch(10, 4, vals, mask, t, status=True, dl=True)
+    assert o["status"][3] & nat.MTG_TRAJ_BAD_TIME
+    assert o["status"][4] & nat.MTG_TRAJ_NOT_SPD and not o["status"][4] & nat.MTG_TRAJ_BAD_TIME
+    assert o["status"][5] & nat.MTG_TRAJ_NOT_SPD
+    assert np.all(o["status"][6:] == 0) and np.all(o["status"][:3] == 0)
+    full = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, status=True, dl=True)["coeffs"]
+    dev = torch.device("cuda:0")
+    dv, dm, dt = (torch.from_numpy(x).to(dev) for x in (vals, mask, times))
+    buf = torch.zeros(full.size + 1, dtype=torch.float64, device=dev)
+    c8 = buf[1:].view(full.shape)  # 8-B aligned, not 16
+    gpu_ctx.solve_linear_batch(10, 4, dv, dm, dt, coeffs=c8, dl=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c8.cpu().numpy(), full)
+    c16 = torch.zeros(full.shape, dtype=torch.float64, device=dev)
+    gpu_ctx.solve_linear_batch(10, 4, dv, dm, dt, coeffs=c16, dl=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c16.cpu().numpy(), full)
