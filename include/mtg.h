@@ -87,7 +87,12 @@ extern "C" {
 #define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10, K = 10, D <= 4, r >= 1;
                                           one lane per (chain, dimension), waves whose masks are not the
                                           reference generators' pattern run the column kernel inside it):
-                                          DESIGN.md 3.2c */
+                                          DESIGN.md 3.2c.  The default for those shapes from
+                                          MTG_DL_MIN_BATCH trajectories on (mtg_solve_kernel_batch) */
+#define MTG_FLAG_COLUMN_KERNEL 128u    /* the register column kernel wherever it applies, also where the
+                                          default for the batch size is the dimension-lane kernel (A/B) */
+#define MTG_DL_MIN_BATCH 16385         /* batches from this size on run the dimension-lane kernel by default
+                                          where it applies (below, the column kernel is as fast) */
 
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
 #define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave
@@ -108,6 +113,9 @@ int mtg_abi_version(void);
 /* The solve kernel (MTG_KERNEL_*) mtg_solve_linear_batch runs for this shape and these flags, or a
    negative MTG_ERR_* for a shape it rejects.  No device work. */
 int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned flags);
+/* The same for a batch of B trajectories (or trajectory x candidate pairs): the default kernel depends
+   on B (MTG_DL_MIN_BATCH); mtg_solve_kernel answers for batches below MTG_DL_MIN_BATCH. */
+int mtg_solve_kernel_batch(int N, int D, int K, int derivative_to_optimize, int64_t B, unsigned flags);
 const char* mtg_status_string(int code);
 const char* mtg_last_error(mtg_ctx* ctx);
 

@@ -34,6 +34,8 @@ MTG_FLAG_GENERAL_KERNEL = 8
 MTG_FLAG_LANE_KERNEL = 16
 MTG_FLAG_IP_KERNEL = 32
 MTG_FLAG_DL_KERNEL = 64
+MTG_FLAG_COLUMN_KERNEL = 128
+MTG_DL_MIN_BATCH = 16385
 
 MTG_KERNEL_LANE = 1
 MTG_KERNEL_COLUMN = 2
@@ -50,6 +52,8 @@ _c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
 _SIGNATURES = {
     "mtg_abi_version": (ctypes.c_int, []),
     "mtg_solve_kernel": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint]),
+    "mtg_solve_kernel_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                              ctypes.c_uint]),
     "mtg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "mtg_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "mtg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
@@ -193,9 +197,11 @@ def check(code, ctx=None):
     return code
 
 
-def solve_kernel(N, D, K, r, flags=0):
-    """Name of the solve kernel mtg_solve_linear_batch runs for this shape (mtg_solve_kernel)."""
-    code = load().mtg_solve_kernel(N, D, K, r, flags)
+def solve_kernel(N, D, K, r, flags=0, B=None):
+    """Name of the solve kernel mtg_solve_linear_batch runs for this shape (mtg_solve_kernel), or for a
+    batch of B trajectories (mtg_solve_kernel_batch: the default depends on B)."""
+    lib = load()
+    code = lib.mtg_solve_kernel(N, D, K, r, flags) if B is None else lib.mtg_solve_kernel_batch(N, D, K, r, B, flags)
     if code < 0:
         raise MTGError(code, status_string(code))
     return KERNEL_NAMES[code]

@@ -482,8 +482,13 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   // (a time sweep passes scales, also with one candidate: it takes the single-stream path, which stages them)
   if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 && !scales &&
       (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes) {
+    // the chunks run the kernel the whole batch would (the default depends on the batch size)
+    const unsigned kf = flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL |
+                                 MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
+    const unsigned pin = mtg::solve_kernel(N, D, K, kf, r, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
+                                                                                     : MTG_FLAG_COLUMN_KERNEL;
     const int rc = run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out,
-                                       cost_out, status, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL | MTG_FLAG_DL_KERNEL));
+                                       cost_out, status, kf | pin);
     if (rc != kPipelineUnavailable) return rc;
   }
   mtg::SolveArgs a{};
@@ -584,7 +589,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL | MTG_FLAG_DL_KERNEL)));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL)));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (pin) {
@@ -626,6 +631,12 @@ int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned f
   if (!mtg::solve_geometry(N, D, K, &lg, &lds, &tpb)) return MTG_ERR_TOO_LARGE;
   if (flags & MTG_FLAG_SPLIT_KERNELS) return MTG_KERNEL_SPLIT;
   return mtg::solve_kernel(N, D, K, flags, derivative_to_optimize);
+}
+
+int mtg_solve_kernel_batch(int N, int D, int K, int derivative_to_optimize, int64_t B, unsigned flags) {
+  const int k = mtg_solve_kernel(N, D, K, derivative_to_optimize, flags);
+  if (k < 0 || k == MTG_KERNEL_SPLIT || B < 0) return k;
+  return mtg::solve_kernel(N, D, K, flags, derivative_to_optimize, B);
 }
 
 const char* mtg_status_string(int code) {
@@ -757,6 +768,11 @@ int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D,
   const int V = K + 1, h = N / 2;
   const size_t s_vals = (size_t)V * h * D, s_coef = (size_t)K * D * N, s_free = (size_t)D * V * h;
   std::vector<int> rcs(n_ctxs, MTG_OK);
+  // every shard runs the kernel the whole batch would on one device (the default depends on the
+  // batch size), so the result does not depend on the number of devices
+  if (!(flags & MTG_FLAG_SPLIT_KERNELS))
+    flags |= mtg::solve_kernel(N, D, K, flags, derivative_to_optimize, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
+                                                                                             : MTG_FLAG_COLUMN_KERNEL;
   auto shard = [&](int g) {
     int64_t b0 = 0, b1 = 0;
     mtg_shard_range(batch, n_ctxs, g, &b0, &b1);

@@ -58,7 +58,8 @@ bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes,
 // the general LDS-resident kernel (mtg_kernels.hip); MTG_FLAG_LANE_KERNEL selects the
 // lane-per-chain kernel (mtg_solve_lane.hip) where lane_geometry allows it, MTG_FLAG_GENERAL_KERNEL
 // the general kernel.
-int solve_kernel(int N, int D, int K, unsigned flags, int r = -1);  // MTG_KERNEL_*
+// B: the batch (trajectories, or trajectory x candidate pairs; < 0: below MTG_DL_MIN_BATCH).
+int solve_kernel(int N, int D, int K, unsigned flags, int r = -1, int64_t B = -1);  // MTG_KERNEL_*
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags = 0);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);
 hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);

@@ -87,7 +87,7 @@ class Context:
         return np.array(buf[:got.value], dtype=np.float64)
 
     def solve_call(self, N, r, values, mask, times, coeffs, free=None, n_free=None, cost=None, status=None,
-                   split=False, general=False, lane=False, ip=False, dl=False):
+                   split=False, general=False, lane=False, ip=False, dl=False, column=False):
         """A zero-argument callable that launches one device-pointer solve asynchronously on the
         current stream with the arguments bound once (the bench's step; minimal host overhead)."""
         import torch
@@ -99,6 +99,7 @@ class Context:
         flags |= nat.MTG_FLAG_LANE_KERNEL if lane else 0
         flags |= nat.MTG_FLAG_IP_KERNEL if ip else 0
         flags |= nat.MTG_FLAG_DL_KERNEL if dl else 0
+        flags |= nat.MTG_FLAG_COLUMN_KERNEL if column else 0
         fn = self._lib.mtg_solve_linear_batch
         args = (self.handle, N, D, K, r, B, _addr(values), _addr(mask), _addr(times), _addr(coeffs), _addr(free),
                 _addr(n_free), _addr(cost), _addr(status), flags)
@@ -149,7 +150,7 @@ class Context:
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
                            cost=None, status=None, split=False, asynchronous=False, general=False, lane=False,
-                           ip=False, dl=False):
+                           ip=False, dl=False, column=False):
         """Solve a batch; returns dict of outputs (allocates those not given).
 
         want-flags: pass arrays (or True to allocate) for free / n_free / cost / status."""
@@ -200,6 +201,8 @@ class Context:
             flags |= nat.MTG_FLAG_IP_KERNEL
         if dl:
             flags |= nat.MTG_FLAG_DL_KERNEL
+        if column:
+            flags |= nat.MTG_FLAG_COLUMN_KERNEL
         rc = self._lib.mtg_solve_linear_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                               _addr(times), _addr(coeffs), _addr(free), _addr(n_free),
                                               _addr(cost), _addr(status), flags)
@@ -207,7 +210,7 @@ class Context:
         return out
 
     def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
-                         asynchronous=False, split=False, ip=False, dl=False):
+                         asynchronous=False, split=False, ip=False, dl=False, column=False):
         dev = _is_torch(values) and values.is_cuda
         B, V, h, D = values.shape
         K = V - 1
@@ -231,6 +234,8 @@ class Context:
             flags |= nat.MTG_FLAG_IP_KERNEL
         if dl:
             flags |= nat.MTG_FLAG_DL_KERNEL
+        if column:
+            flags |= nat.MTG_FLAG_COLUMN_KERNEL
         rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                             _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
         nat.check(rc, self.handle)

@@ -20,7 +20,8 @@ out = torch.empty((max(Bs), 10, 3, 10), dtype=torch.float64, device=dev)
 ctx = mtg.Context(0)
 for B in Bs:
     row = {"B": B}
-    kinds = (("lane", {"lane": True}), ("column", {}), ("ip", {"ip": True}), ("dl", {"dl": True}))
+    kinds = (("lane", {"lane": True}), ("column", {"column": True}), ("ip", {"ip": True}), ("dl", {"dl": True}),
+             ("default", {}))
     for name, kw in [k for k in kinds if k[0] in os.environ.get("KERNELS", "lane,column").split(",")]:
         step = ctx.solve_call(10, 4, v_d[:B], m_d[:B], t_d[:B], out[:B], **kw)
         ctx.enable_timing(0)

@@ -139,6 +139,19 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_SPLIT_KERNELS) == split
     assert lib.mtg_solve_kernel(10, 3, 13, 4, 0) == gen
+    # the batch-size-aware query: the dimension-lane kernel by default from MTG_DL_MIN_BATCH on, where
+    # it applies (N = 10, K = 10, D <= 4, r >= 1); the column flag keeps the column kernel
+    dl = nat.MTG_KERNEL_DL
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10000, 0) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH - 1, 0) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH, 0) == dl
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 125000, nat.MTG_FLAG_COLUMN_KERNEL) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10, nat.MTG_FLAG_DL_KERNEL) == dl
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 0, 125000, 0) == col  # r = 0: no translation trick
+    assert lib.mtg_solve_kernel_batch(10, 3, 8, 4, 125000, 0) == col   # K != 10
+    assert lib.mtg_solve_kernel_batch(12, 3, 20, 3, 125000, 0) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 125000, nat.MTG_FLAG_SPLIT_KERNELS) == split
+    assert nat.solve_kernel(10, 3, 10, 4, B=125000) == "solve_dl_kernel"
     assert lib.mtg_solve_kernel(10, 3, 50, 4, 0) == gen
     assert lib.mtg_solve_kernel(11, 3, 10, 4, 0) == nat.MTG_ERR_UNSUPPORTED_N
     assert lib.mtg_solve_kernel(10, 3, 10, 5, 0) == nat.MTG_ERR_BAD_DERIVATIVE

@@ -537,10 +537,11 @@ def test_g_in_lds_and_register_paths_bitwise_equal(gpu_ctx):
     dev = torch.device("cuda", 0)
     v_d, m_d, t_d = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (vals, mask, times))
     c_d = torch.empty((big, 10, 3, 10), dtype=torch.float64, device=dev)
-    gpu_ctx.solve_call(10, 4, v_d, m_d, t_d, c_d)()
+    # (the column kernel at both sizes: from MTG_DL_MIN_BATCH on the default is the DL kernel)
+    gpu_ctx.solve_call(10, 4, v_d, m_d, t_d, c_d, column=True)()
     torch.cuda.synchronize()
     whole = c_d.cpu().numpy()
-    part = gpu_ctx.solve_linear_batch(10, 4, vals[:777], mask[:777], times[:777])
+    part = gpu_ctx.solve_linear_batch(10, 4, vals[:777], mask[:777], times[:777], column=True)
     np.testing.assert_array_equal(part["coeffs"], whole[:777])
     np.testing.assert_array_equal(part["coeffs"][-1], whole[776])
 
