@@ -38,6 +38,7 @@
 // sweep, which also recovers coefficients and the cost and streams them to HBM.
 // Everything is FP64 (the reference is FP64 throughout).
 #include "mtg_device.h"
+#include "mtg_fused.inc"
 
 #include <stdlib.h>
 
@@ -45,310 +46,8 @@ namespace mtg {
 
 template <int N, int R>
 __global__ __launch_bounds__(kBlock) void solve_fused_kernel(SolveArgs a, int lg_log2) {
-  constexpr int H = N / 2;
-  constexpr unsigned HMASK = (1u << H) - 1u;
   extern __shared__ __attribute__((aligned(16))) double lds[];
-
-  const int LG = 1 << lg_log2;
-  const int lane = threadIdx.x;
-  const int slot = lane >> lg_log2;
-  const int c = lane & (LG - 1);
-  const int tpb = kBlock >> lg_log2;
-  const int64_t pair = (int64_t)blockIdx.x * tpb + slot;
-  const bool valid = pair < a.B;
-  const int K = a.K, V = K + 1, D = a.D;
-  const bool is_g = c < H;
-  const bool is_d = (c >= H) && (c < H + D);
-  const int d = is_d ? c - H : 0;
-  const int cs = is_g ? c : 0;
-  const int64_t pb = valid ? pair : 0;
-  const int64_t tb = pb / a.n_cand;
-  const double tscale = a.scales ? a.scales[pb % a.n_cand] : 1.0;
-
-  double* xs = lds + (size_t)slot * slot_doubles(H, D, K, LG);
-  double* gst = xs + LG * H;
-  double* zst = gst + K * H * H;
-
-  const double* Ht = c_htilde + MTG_HTILDE_OFF(N, R);
-  const double* vals = a.values + tb * (int64_t)V * H * D;
-  const uint8_t* msk = a.mask + tb * V;
-  const double* tms = a.times + tb * K;
-
-  // ---- forward block-Thomas sweep on the symmetrically pinned system (fixed rows AND columns
-  // of R replaced by the identity, fixed values moved to the right-hand side):
-  //   S_v = D_v - E_{v-1}^T G_{v-1},  [G_v | z_v] = S_v^-1 [E_v | rhs_v],
-  //   rhs_v = -(D_v xf_v + E_{v-1}^T (xf_{v-1} + z_{v-1}) + E_v xf_{v+1})   (free rows).
-  // Every lane runs the same four mat-vecs against Htilde per vertex with its own inputs:
-  //   column lane c:  a1 = e_c (column c of D_v), a2 = -g_{v-1}, a3 = e_c (column c of E_v)
-  //   dim lane d:     a1 = xf_v, a2 = xf_{v-1} + z_{v-1}, a3 = xf_{v+1}
-  int st = 0, n_free = 0;
-  double pmin = DBL_MAX;
-  double gp[H], xfc[H], xfn[H];
-#pragma unroll
-  for (int k = 0; k < H; ++k) gp[k] = 0.0;
-  double sp[H], scp = 0.0, sn[H], scn = 0.0;
-#pragma unroll
-  for (int k = 0; k < H; ++k) sp[k] = 0.0;
-  {
-    const double T0 = tms[0] * tscale;
-    st |= time_bits(T0);
-    seg_powers<H, R>(T0, sn, scn);
-  }
-  unsigned raw = msk[0];
-  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned m_cur = raw & HMASK;
-  raw = msk[1];
-  if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-  unsigned m_next = raw & HMASK;
-  unsigned m_prev = 0;
-  double xfp0 = 0.0;  // fixed position of vertex v-1 (dim lanes)
-  load_fixed<H>(vals, 0, D, d, m_cur, xfc);
-  load_fixed<H>(vals, 1, D, d, m_next, xfn);
-  for (int v = 0; v < V; ++v) {
-    const bool has_prev = v > 0, has_next = v < K;
-    cdouble* Hs = launder(Ht);
-    const bool c_free = !((m_cur >> cs) & 1u);
-    const bool c_free_next = !((m_next >> cs) & 1u);
-    double a1[H], a2[H], a3[H];
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      const double ek = (k == c) ? 1.0 : 0.0;
-      a1[k] = is_g ? (c_free ? ek : 0.0) : xfc[k];
-      a2[k] = gp[k];  // column lanes keep -g_{v-1}, dim lanes xf_{v-1} + z_{v-1}
-      a3[k] = is_g ? (c_free_next ? ek : 0.0) : xfn[k];
-    }
-    // Translation invariance (r >= 1: H_i [1 0..0 1 0..0]^T = 0): for a segment whose two end
-    // positions are both fixed, the fixed-value products use positions relative to the segment
-    // start.  Exact in real arithmetic; in FP64 it removes the cancellation of
-    // H^TL p_v + H^TR p_{v+1} on short segments (up to 500x more accurate, DESIGN.md "Numerics").
-    double a1b0 = a1[0];
-    if (R >= 1 && is_d) {
-      const bool pos_c = m_cur & 1u, pos_p = m_prev & 1u, pos_n = m_next & 1u;
-      if (has_prev && pos_p && pos_c) {  // segment v-1: positions relative to p_{v-1}
-        a1b0 = xfc[0] - xfp0;
-        a2[0] = 0.0;
-      }
-      if (has_next && pos_c && pos_n) {  // segment v: positions relative to p_v
-        a3[0] = xfn[0] - xfc[0];
-        a1[0] = 0.0;
-      }
-    }
-    double m[H], y[H];
-#pragma unroll
-    for (int i = 0; i < H; ++i) m[i] = 0.0, y[i] = 0.0;
-    if (has_prev) {  // bottom rows of H_{v-1}: [BL | BR] [a2; a1]
-      double u[N];
-#pragma unroll
-      for (int k = 0; k < H; ++k) u[k] = sp[k] * a2[k], u[H + k] = sp[k] * a1[k];
-      u[H] = a1b0;  // sp[0] == 1
-#pragma unroll
-      for (int i = 0; i < H; ++i) {
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < N; ++j) t += Hs[(H + i) * N + j] * u[j];
-        m[i] = scp * sp[i] * t;
-      }
-    }
-    if (has_next) {  // top rows of H_v: TL a1 and TR a3
-      double w1[H], w3[H];
-#pragma unroll
-      for (int k = 0; k < H; ++k) w1[k] = sn[k] * a1[k], w3[k] = sn[k] * a3[k];
-#pragma unroll
-      for (int i = 0; i < H; ++i) {
-        double t1 = 0.0, t3 = 0.0;
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-          t1 += Hs[i * N + j] * w1[j];
-          t3 += Hs[i * N + H + j] * w3[j];
-        }
-        const double f = scn * sn[i];
-        m[i] += f * t1;
-        y[i] = f * t3;
-      }
-    }
-    double rhs[H];
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const bool fi = !((m_cur >> i) & 1u);
-      double sv = c_free ? (fi ? m[i] : 0.0) : (i == c ? 1.0 : 0.0);
-      double rg = fi ? y[i] : 0.0;
-      double rd = fi ? -(m[i] + y[i]) : 0.0;
-      asm volatile("" : "+v"(sv), "+v"(rg), "+v"(rd));  // all computed: branch-free selects
-      xs[c * H + i] = sv;  // only columns c < H are read
-      rhs[i] = is_g ? rg : rd;
-    }
-    __syncthreads();
-    double S[H][H];
-#pragma unroll
-    for (int i = 0; i < H; ++i)
-#pragma unroll
-      for (int j = 0; j <= i; ++j) S[i][j] = xs[j * H + i];
-    __syncthreads();
-    double dinv[H], x[H];
-    const double pv = ldlt<H>(S, dinv);
-    pmin = (pv < pmin || pv != pv) ? pv : pmin;  // a NaN pivot sticks (NOT_SPD)
-    ldlt_solve<H>(S, dinv, rhs, x);
-    if (is_g && has_next) {
-#pragma unroll
-      for (int i = 0; i < H; ++i) gst[(v * H + c) * H + i] = x[i];
-    }
-    if (is_d) {
-#pragma unroll
-      for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i];
-    }
-#pragma unroll
-    for (int i = 0; i < H; ++i) gp[i] = is_g ? -x[i] : xfc[i] + x[i];
-    n_free += __builtin_popcount(~m_cur & HMASK);
-    if (has_next) {
-      xfp0 = xfc[0];
-      m_prev = m_cur;
-#pragma unroll
-      for (int k = 0; k < H; ++k) sp[k] = sn[k], xfc[k] = xfn[k];
-      scp = scn;
-      m_cur = m_next;
-      if (v + 1 < K) {
-        const double Tn = tms[v + 1] * tscale;
-        st |= time_bits(Tn);
-        seg_powers<H, R>(Tn, sn, scn);
-        raw = msk[v + 2];
-        if (raw & ~HMASK) st |= MTG_TRAJ_WARN_DROPPED;
-        m_next = raw & HMASK;
-        load_fixed<H>(vals, v + 2, D, d, m_next, xfn);
-      } else {
-        m_next = 0;
-#pragma unroll
-        for (int k = 0; k < H; ++k) xfn[k] = 0.0;
-      }
-    }
-  }
-  if (!(pmin > 0.0 && pmin <= DBL_MAX)) st |= MTG_TRAJ_NOT_SPD;
-  __syncthreads();
-
-  // ---- backward substitution (dimension lanes): x_v = z_v - G_v x_{v+1}, kept in Z
-  if (is_d) {
-    double xn[H];
-#pragma unroll
-    for (int k = 0; k < H; ++k) xn[k] = zst[(K * D + d) * H + k];
-    for (int v = K - 1; v >= 0; --v) {
-      double x[H];
-#pragma unroll
-      for (int i = 0; i < H; ++i) x[i] = zst[(v * D + d) * H + i];
-#pragma unroll
-      for (int cc = 0; cc < H; ++cc) {
-        const double xc = xn[cc];
-#pragma unroll
-        for (int i = 0; i < H; ++i) x[i] -= gst[(v * H + cc) * H + i] * xc;
-      }
-#pragma unroll
-      for (int i = 0; i < H; ++i) zst[(v * D + d) * H + i] = x[i], xn[i] = x[i];
-    }
-  }
-  __syncthreads();
-
-  // ---- epilogue: coefficients c = diag(T^-j) A(1)^-1 S(T) [x_i; x_{i+1}] and the cost, items (i, d)
-  double cacc = 0.0;
-  // Items (segment i, dimension dd) go in rounds of LG, item it = base + c.  A round's coefficient
-  // rows are consecutive in HBM ([K][D][N] per trajectory): when the G store (dead after the
-  // backward sweep) can hold them they are staged there and stored as one contiguous run per
-  // trajectory, 16 B per lane at consecutive addresses (per-lane 16-B pieces at an N-double
-  // stride kept the store unit busy for most of the epilogue; see mtg_solve_reg.inc).
-  const bool stage = K * H * H >= LG * N && !(slot_doubles(H, D, K, LG) & 1);  // room, 16-B aligned
-  for (int base = 0; base < K * D; base += LG) {
-    const int it = base + c;
-    const bool have = it < K * D;
-    const int i = have ? it / D : 0, dd = have ? it - i * D : 0;
-    cdouble* Hl = launder(c_htilde + MTG_HTILDE_OFF(N, R));
-    cdouble* Ai1 = launder(c_a1inv + MTG_A1INV_OFF(N));
-    const double T = tms[i] * tscale;
-    double s[H], sc;
-    seg_powers<H, R>(T, s, sc);
-    double x0[H], x1[H];
-    load_fixed<H>(vals, i, D, dd, msk[i], x0);
-    load_fixed<H>(vals, i + 1, D, dd, msk[i + 1], x1);
-    double sh[N];
-#pragma unroll
-    for (int k = 0; k < H; ++k) {
-      sh[k] = s[k] * (x0[k] + zst[(i * D + dd) * H + k]);
-      sh[H + k] = s[k] * (x1[k] + zst[((i + 1) * D + dd) * H + k]);
-    }
-    // the polynomial of [x_i - p 1; x_{i+1} - p 1] is p(t) - p: recover it relative to the start
-    // position p (only c_0 changes), which avoids cancelling p_i against p_{i+1} in c_j, j >= h
-    const double p0 = sh[0];
-    sh[0] = 0.0;
-    sh[H] -= p0;
-    if (a.coeffs) {
-      const double tinv = rcp(T);
-      double out[N];
-      double tp = 1.0;
-#pragma unroll
-      for (int j = 0; j < N; ++j) {
-        double acc;
-        if (j < H) {  // A(1)^-1 top-left = diag(1/j!), top-right = 0
-          acc = (j == 0) ? p0 : Ai1[j * N + j] * sh[j];
-        } else {
-          acc = 0.0;
-#pragma unroll
-          for (int q = 0; q < N; ++q) acc += Ai1[j * N + q] * sh[q];
-        }
-        out[j] = acc * tp;
-        tp *= tinv;
-      }
-      if (stage) {
-        double2* o2 = reinterpret_cast<double2*>(gst + c * N);
-#pragma unroll
-        for (int j = 0; j < N / 2; ++j) o2[j] = make_double2(out[2 * j], out[2 * j + 1]);
-        __syncthreads();  // (one wave per block: orders the LDS staging)
-        const int nrun = (K * D - base < LG ? K * D - base : LG) * (N / 2);  // double2s this round
-        if (valid) {
-          double2* dst = reinterpret_cast<double2*>(a.coeffs + (pb * (K * D) + base) * N);
-          const double2* src = reinterpret_cast<const double2*>(gst);
-          for (int e = c; e < nrun; e += LG) store_stream(dst + e, src[e]);
-        }
-        __syncthreads();
-      } else if (valid && have) {
-        double2* dst = reinterpret_cast<double2*>(a.coeffs + ((pb * K + i) * D + dd) * N);
-#pragma unroll
-        for (int j = 0; j < N / 2; ++j) store_stream(dst + j, make_double2(out[2 * j], out[2 * j + 1]));
-      }
-    }
-    if (a.cost_out && have) {  // 0.5 c^T Q c = 0.5 sc sh^T Htilde sh  (translation-invariant for r >= 1)
-      if (R == 0) sh[0] = p0, sh[H] += p0;
-      double q = 0.0;
-#pragma unroll
-      for (int p = 0; p < N; ++p) {
-        double row = 0.5 * Hl[p * N + p] * sh[p];
-#pragma unroll
-        for (int t = p + 1; t < N; ++t) row += Hl[p * N + t] * sh[t];
-        q += sh[p] * row;
-      }
-      cacc += sc * q;
-    }
-  }
-  // free derivatives in the reference order (sorted by vertex, then derivative)
-  if (a.free_out && valid && is_d) {
-    double* fo = a.free_out + (pb * D + d) * ((int64_t)V * H);
-    int idx = 0;
-    for (int v = 0; v < V; ++v) {
-      const unsigned mv = msk[v] & HMASK;
-#pragma unroll
-      for (int k = 0; k < H; ++k)
-        if (!((mv >> k) & 1u)) fo[idx++] = zst[(v * D + d) * H + k];
-    }
-  }
-  if (a.cost_out) {  // fixed-order reduction over the group's lanes (deterministic)
-    __syncthreads();
-    xs[c] = cacc;
-    __syncthreads();
-    if (c == 0 && valid) {
-      double tot = 0.0;
-      for (int q = 0; q < LG; ++q) tot += xs[q];
-      a.cost_out[pb] = tot;
-    }
-  }
-  if (c == 0 && valid) {
-    if (a.status) a.status[pb] = st;
-    if (a.n_free_out) a.n_free_out[pb] = n_free;
-  }
+  solve_fused_block<N, R>(a, lg_log2, (int64_t)blockIdx.x * (kBlock >> lg_log2), lds);
 }
 
 bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes, int* traj_per_block) {

@@ -10,14 +10,13 @@ namespace mtg {
 MTG_DL_DECL(10, 1) MTG_DL_DECL(10, 2) MTG_DL_DECL(10, 3) MTG_DL_DECL(10, 4)
 #undef MTG_DL_DECL
 
-// Shapes the kernel serves: N = 10, K = 10, D <= 4, r >= 1 (translation-relative positions), with
-// the column kernel's geometry for the waves of other patterns.
+// Shapes the kernel serves: N = 10, K = 10, D <= 4, r >= 1 (translation-relative positions), within
+// 64 KB of LDS for its own path and for the general kernel's block function (the waves of other
+// patterns).
 bool dl_geometry(int N, int D, int K, int r) {
   if (N != 10 || K != 10 || D < 1 || D > 4 || r < 1 || r > N / 2 - 1) return false;
-  int lg;
-  size_t lds;
-  if (!reg_geometry(N, D, K, &lg, &lds)) return false;
-  return sizeof(double) * (size_t)dl_lds_doubles(N, D, K) <= kMaxLdsPerBlock;
+  const size_t fb = sizeof(double) * (size_t)kDlFallbackTraj * slot_doubles(N / 2, D, K, 1 << kDlFallbackLgLog2);
+  return sizeof(double) * (size_t)dl_lds_doubles(N, D, K) <= kMaxLdsPerBlock && fb <= kMaxLdsPerBlock;
 }
 
 // Trajectories per wave: all 64 / (2 D) the lanes hold, unless MTG_DL_TPW asks for fewer (A/B).

@@ -971,7 +971,7 @@ def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
     the two kernels, which the conditioning of R_pp amplifies to ~3e-10: 1e-9), the column kernel
     (1e-8, scale-normalised: the host path and the oracle differ by up to 1.4e-8 on these batches) and
     the oracle; free values, n_free, cost and status; a ragged last wave; a wave whose masks break the
-    pattern runs the column kernel's block function inside it, bit-identical to it."""
+    pattern runs the general kernel's block function inside it, bit-identical to it."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
     O = _oracle()
@@ -1002,7 +1002,7 @@ def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
     m2 = mask.copy()
     m2[2 * tpw + 1, 2] |= 2
     dl2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, dl=True, **kw)
-    col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, **kw)
+    col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, general=True, **kw)
     w = slice(2 * tpw, 3 * tpw)
     for k in ("coeffs", "cost", "free", "status"):
         np.testing.assert_array_equal(dl2[k][w], col2[k][w], err_msg=k)
