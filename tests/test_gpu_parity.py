@@ -1005,7 +1005,10 @@ def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
     col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, general=True, **kw)
     w = slice(2 * tpw, 3 * tpw)
     for k in ("coeffs", "cost", "free", "status"):
-        np.testing.assert_array_equal(dl2[k][w], col2[k][w], err_msg=k)
+        if k == "cost":  # (the general kernel sums the cost over its 8 or 16 lanes: 1-ulp differences)
+            np.testing.assert_allclose(dl2[k][w], col2[k][w], rtol=1e-14, err_msg=k)
+        else:
+            np.testing.assert_array_equal(dl2[k][w], col2[k][w], err_msg=k)
         np.testing.assert_array_equal(dl2[k][:2 * tpw], dl[k][:2 * tpw], err_msg=k)
         np.testing.assert_array_equal(dl2[k][3 * tpw:], dl[k][3 * tpw:], err_msg=k)
 
