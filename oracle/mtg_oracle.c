@@ -110,6 +110,12 @@ static void base_init(void) {
   g_base_init = 1;
 }
 
+/* The table is filled once, before any parallel region reads it: a lazy first fill from inside an
+ * OpenMP loop let one thread's memset run while another thread, seeing g_base_init already set,
+ * read the half-rebuilt table (a fresh process's first multi-threaded call could return wrong
+ * coefficients: one smoke run saw a 1.5 scale-normalised error against correct GPU results). */
+__attribute__((constructor)) static void base_ctor(void) { base_init(); }
+
 double oracle_base_coefficient(int n, int i) {
   base_init();
   if (n < 0 || i < 0 || n >= BASE_N || i >= BASE_N) return 0.0;
@@ -533,6 +539,7 @@ int oracle_solve_linear_batch(int N, int D, int K, int r, int nd, int64_t B, con
   const int V = K + 1;
   int err = 0;
 #ifdef _OPENMP
+  base_init(); /* (before the parallel region: see base_ctor) */
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 16) reduction(| : err)
 #endif
@@ -632,6 +639,7 @@ int oracle_cost_at_times_batch(int N, int D, int K, int r, int nd, int64_t B, co
   if (N < 2 || N > ORACLE_KMAXN || (N % 2) || K < 1 || D < 1 || C < 1 || nd < N / 2) return ORACLE_ERR_ARG;
   const int V = K + 1;
 #ifdef _OPENMP
+  base_init(); /* (before the parallel region: see base_ctor) */
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 4)
 #endif
@@ -662,6 +670,7 @@ int oracle_cost_time_jacobian_batch(int N, int D, int K, int r, int nd, int64_t 
     return ORACLE_ERR_ARG;
   const int V = K + 1;
 #ifdef _OPENMP
+  base_init(); /* (before the parallel region: see base_ctor) */
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 4)
 #endif

@@ -4,7 +4,7 @@
 # Each step time-limited; the first failure ends it.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03c
+O=gpurun_out/${EVID:-r03c}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
@@ -15,6 +15,6 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --column-kernel > $O/bench_c
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_20_5.json 2> $O/bench_20_5.err || exit 1
 timeout -k 10 300 python bench.py --batch 125000 --steps 100 --warmup 50 --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
 timeout -k 10 300 python bench.py --batch 125000 --steps 100 --warmup 50 --no-cpu-baseline --column-kernel > $O/bench_c3_column.json 2> $O/bench_c3_column.err || exit 1
-bash scripts/profile.sh 10000 "" _c2dlf || exit $?
-bash scripts/profile.sh 125000 "" _c3dlf || exit $?
+bash scripts/profile.sh 10000 "" _c2dl${EVID:-f} || exit $?
+bash scripts/profile.sh 125000 "" _c3dl${EVID:-f} || exit $?
 echo OK > $O/done
