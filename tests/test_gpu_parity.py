@@ -1045,3 +1045,18 @@ def test_dl_kernel_time_sweep_status_and_device_outputs(gpu_ctx):
     gpu_ctx.solve_linear_batch(10, 4, dv, dm, dt, coeffs=c16, dl=True)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(c16.cpu().numpy(), full)
+
+
+def test_time_sweep_large_default_runs_dl(gpu_ctx):
+    """A time sweep of 200 trajectories x 64 candidates (12800 pairs: the DL kernel by default, from
+    MTG_DL_MIN_BATCH on) equals the column kernel's sweep (rtol 1e-9) and re-solves at scaled times."""
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    assert nat.solve_kernel(10, 3, 10, 4, B=200 * 64) == "solve_dl_kernel"
+    vals, mask, times = _bench_batch(200, seed0=61)
+    scales = 0.5 + np.arange(64) / 63.0
+    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales)
+    Jc = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, column=True)
+    np.testing.assert_allclose(J, Jc, rtol=1e-9, atol=0)
+    for ci in (0, 31, 63):
+        ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times * scales[ci], cost=True)["cost"]
+        np.testing.assert_allclose(J[:, ci], ref, rtol=1e-9, atol=0)
