@@ -91,9 +91,9 @@ extern "C" {
                                           MTG_DL_MIN_BATCH trajectories on (mtg_solve_kernel_batch) */
 #define MTG_FLAG_COLUMN_KERNEL 128u    /* the register column kernel wherever it applies, also where the
                                           default for the batch size is the dimension-lane kernel (A/B) */
-#define MTG_DL_MIN_BATCH 9216          /* batches from this size on run the dimension-lane kernel by default
-                                          where it applies (below, fewer than ~one of its waves per SIMD: the
-                                          column kernel is faster) */
+#define MTG_DL_MIN_BATCH 2048          /* batches from this size on run the dimension-lane kernel by default
+                                          where it applies (measured faster from 2048 on; below, both kernels
+                                          are one wave's latency) */
 
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
 #define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave

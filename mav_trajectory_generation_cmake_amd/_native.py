@@ -35,7 +35,7 @@ MTG_FLAG_LANE_KERNEL = 16
 MTG_FLAG_IP_KERNEL = 32
 MTG_FLAG_DL_KERNEL = 64
 MTG_FLAG_COLUMN_KERNEL = 128
-MTG_DL_MIN_BATCH = 9216
+MTG_DL_MIN_BATCH = 2048
 
 MTG_KERNEL_LANE = 1
 MTG_KERNEL_COLUMN = 2

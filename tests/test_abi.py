@@ -142,7 +142,8 @@ def test_solve_kernel_selection():
     # the batch-size-aware query: the dimension-lane kernel by default from MTG_DL_MIN_BATCH on, where
     # it applies (N = 10, K = 10, D <= 4, r >= 1); the column flag keeps the column kernel
     dl = nat.MTG_KERNEL_DL
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 8192, 0) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 1024, 0) == col
+    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 8192, 0) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10000, 0) == dl  # config 2
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH - 1, 0) == col
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH, 0) == dl

@@ -285,13 +285,15 @@ def _bench_batch_d(B, D, seed0=0, K=10, N=10):
 
 @pytest.mark.parametrize("path", ["default", "split"])
 def test_time_sweep_matches_solves(gpu_ctx, path):
-    """mtg_time_sweep_batch == computeCost of separate solves at scaled times."""
+    """mtg_time_sweep_batch == computeCost of separate solves at scaled times, with the same kernel
+    (the 4096 pairs would run the DL kernel by default and the 64-trajectory solves the column kernel:
+    the column kernel for both here; the DL kernel's sweep: test_time_sweep_large_default_runs_dl)."""
     B = 64
     vals, mask, times = _bench_batch(B, seed0=3)
     scales = 0.5 + np.arange(64) / 63.0
-    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, split=(path == "split"))
+    J = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, split=(path == "split"), column=True)
     for ci in (0, 17, 63):
-        ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times * scales[ci], cost=True)["cost"]
+        ref = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times * scales[ci], cost=True, column=True)["cost"]
         np.testing.assert_allclose(J[:, ci], ref, rtol=1e-12, atol=0)
 
 
