@@ -17,8 +17,10 @@ Other workloads (--workload), each its own JSON line:
            (getCostAndGradientDerivative + getCostAndGradientTime's J_d gradient at T_c = s_c T,
            s_c = 0.5 + c/63; mtg_time_jacobian_batch, v_mfma_f64_16x16x4_f64)
 
-Multi-GPU: one process per GPU (torchrun), contiguous shards, no data-path
-collective ("scaling": "weak"); a barrier + MAX-over-ranks of the timed region.
+Multi-GPU: one process per GPU, contiguous shards, no data-path collective ("scaling": "weak");
+a barrier + MAX-over-ranks of the timed region.  Under torch.distributed.run the launcher's
+WORLD_SIZE must equal --gpus; without one, `bench.py --gpus N` starts the N rank processes itself
+(self_launch) before anything touches the GPU.
 
 Prints ONE JSON line (rank 0).  Also reports the dominant kernel's roofline
 (algorithmic bytes / measured kernel time vs 8 TB/s HBM peak) and the CPU
@@ -199,6 +201,58 @@ def end_to_end(ctx, N, r, values, mask, times, unit, h2d_bytes, d2h_bytes, n=30)
     return res
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n, port, base_env=None):
+    """The environment of each of the n ranks a self-launched `bench.py --gpus n` starts: what
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_*),
+    rendezvous on 127.0.0.1."""
+    base = dict(os.environ if base_env is None else base_env)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def self_launch(n, argv, cmd=None, popen=None):
+    """`bench.py --gpus n` without an outer launcher: start n rank processes (this script again, same
+    arguments) and wait for them.  Called before anything touches the GPU -- this process imports
+    neither torch nor the library -- so the children are started from a process with no HIP state.
+    Rank 0's JSON line reaches stdout through the inherited descriptor.  If any rank fails the others
+    are stopped and the first failing exit code is returned."""
+    import subprocess
+    if popen is None:
+        popen = subprocess.Popen
+    if cmd is None:
+        cmd = [sys.executable, os.path.abspath(__file__)]
+    procs = [popen(cmd + list(argv), env=e) for e in rank_envs(n, _free_port())]
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:
+                    q.kill()
+        if pending:
+            time.sleep(0.05)
+    return rc
+
+
 def make_problems(workload, N, K, B, seed0):
     import mav_trajectory_generation_cmake_amd as mtg
     if workload == "config4":
@@ -239,6 +293,13 @@ def main():
     ap.add_argument("--column-kernel", action="store_true",
                     help="the register column kernel where it applies, whatever the batch size (A/B)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:  # no outer launcher: one process per GPU, started from here
+            sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks"
+                 % (args.gpus, os.environ["WORLD_SIZE"]))
 
     import torch
     import torch.distributed as dist

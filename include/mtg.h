@@ -299,17 +299,22 @@ int mtg_kernel_times(mtg_ctx* ctx, float* ms, int n, int* n_out);
  * than the solve itself): the C++ drop-in PolynomialOptimization<N>::solveLinear uses it by
  * default (BASELINE config 1), replacing the reference's CPU solveLinear (lin_impl:329-369).
  * Same arrays and per-trajectory status as mtg_solve_linear_batch, all host pointers;
- * threads <= 0: one per hardware thread. */
+ * threads <= 0: mtg_host_default_threads(). */
 int mtg_host_solve_linear_batch(int N, int D, int K, int derivative_to_optimize, int64_t batch,
                                 const double* values, const uint8_t* fixed_mask, const double* times,
                                 double* coeffs, double* free_out, int32_t* n_free_out, double* cost_out,
                                 int32_t* status, int threads);
 
+/* The worker count the host paths (mtg_host_*) use when called with threads <= 0: the CPUs this
+ * process may run on -- its affinity mask, capped by the cgroup CPU quota -- not every CPU of the
+ * machine.  (The reference's host code is single-threaded; there is no reference counterpart.) */
+int mtg_host_default_threads(void);
+
 /* Host (CPU) path of mtg_min_max_magnitude_batch, no context and no GPU needed: the same candidates,
  * root isolation and tie rules as the HIP kernel, on the calling thread(s).  The reference computes
  * Trajectory::computeMinMaxMagnitude on the CPU (src/trajectory.cpp:181-218); the C++ drop-in uses
  * this for its single trajectories unless ExecutionPolicy::kDevice.  All host pointers; threads <= 0:
- * one per hardware thread. */
+ * mtg_host_default_threads(). */
 int mtg_host_min_max_magnitude_batch(int N, int D, int K, int64_t batch, const double* coeffs, const double* times,
                                      int derivative, uint32_t dimension_mask, mtg_extremum* minimum,
                                      mtg_extremum* maximum, int threads);

@@ -102,6 +102,7 @@ _SIGNATURES = {
     "mtg_host_solve_linear_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                    ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
                                                    _c_dp, _c_dp, ctypes.c_int]),
+    "mtg_host_default_threads": (ctypes.c_int, []),
     "mtg_host_min_max_magnitude_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                                         _c_dp, _c_dp, ctypes.c_int, ctypes.c_uint32, _c_dp, _c_dp,
                                                         ctypes.c_int]),

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "mtg.h"
+#include "mtg_host_threads.h"
 
 namespace {
 
@@ -145,7 +146,7 @@ void pack(const Gen& g, int N, double* values, uint8_t* mask) {
 
 template <typename F>
 void parallel_for(int64_t n, int threads, F f) {
-  int t = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int t = threads > 0 ? threads : mtg::usable_cpus();
   t = (int)std::min<int64_t>(t, std::max<int64_t>(1, n / 64));
   if (t <= 1) {
     for (int64_t i = 0; i < n; ++i) f(i);

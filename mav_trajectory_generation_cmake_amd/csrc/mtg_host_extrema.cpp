@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "mtg.h"
+#include "mtg_host_threads.h"
 
 namespace {
 
@@ -140,7 +141,7 @@ extern "C" int mtg_host_min_max_magnitude_batch(int N, int D, int K, int64_t bat
       one(N, D, K, coeffs + b * sc, times + b * K, derivative, dims, minimum ? minimum + b : nullptr,
           maximum ? maximum + b : nullptr);
   };
-  int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+  int nt = threads > 0 ? threads : mtg::usable_cpus();
   if (nt < 1) nt = 1;
   if ((int64_t)nt > batch) nt = (int)batch;
   if (nt == 1) {

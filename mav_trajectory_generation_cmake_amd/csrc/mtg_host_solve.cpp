@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "mtg.h"
+#include "mtg_host_threads.h"
 #include "mtg_tables.inc"
 
 namespace {
@@ -339,6 +340,8 @@ SolveFn solver_for(int N) {
 
 }  // namespace
 
+extern "C" int mtg_host_default_threads(void) { return mtg::usable_cpus(); }
+
 extern "C" int mtg_host_solve_linear_batch(int N, int D, int K, int derivative_to_optimize, int64_t batch,
                                            const double* values, const uint8_t* fixed_mask, const double* times,
                                            double* coeffs, double* free_out, int32_t* n_free_out,
@@ -357,7 +360,7 @@ extern "C" int mtg_host_solve_linear_batch(int N, int D, int K, int derivative_t
                           n_free_out ? n_free_out + b : nullptr, cost_out ? cost_out + b : nullptr, s);
     if (status) status[b] = st;
   };
-  int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+  int nt = threads > 0 ? threads : mtg::usable_cpus();
   if (nt < 1) nt = 1;
   if ((int64_t)nt > batch) nt = (int)batch;
   if (nt == 1) {

@@ -38,8 +38,9 @@ def falling(n, i):
     return out
 
 
-def truth_solve(N, r, vals, mask, times):
-    """60-digit evaluation of the reference algorithm (see module doc)."""
+def _system(N, r, vals, mask, times):
+    """R = M^T H M of the reference (lin_impl:298-326) at 60 digits, with the fixed/free split and the
+    per-segment A^-1 and Q."""
     mp.mp.dps = DPS
     h = N // 2
     V, nd, D = vals.shape
@@ -71,6 +72,15 @@ def truth_solve(N, r, vals, mask, times):
         for a in range(N):
             for b in range(N):
                 R[cols[a]][cols[b]] += H[a, b]
+    return R, fixed, free, col, Ainvs, Qs
+
+
+def truth_solve(N, r, vals, mask, times):
+    """60-digit evaluation of the reference algorithm (see module doc)."""
+    h = N // 2
+    V, nd, D = vals.shape
+    K = V - 1
+    R, fixed, free, col, Ainvs, Qs = _system(N, r, vals, mask, times)
     nf, npf = len(fixed), len(free)
     df = [[mp.mpf(float(vals[v, k, d])) for (v, k) in fixed] for d in range(D)]
     dp = [[mp.mpf(0)] * npf for _ in range(D)]
@@ -93,6 +103,43 @@ def truth_solve(N, r, vals, mask, times):
     free_out = np.array([[float(x) for x in dp[d]] for d in range(D)]).reshape(D, npf)
     fixed_out = np.array([[float(x) for x in df[d]] for d in range(D)]).reshape(D, nf)
     return coeffs, float(cost / 2), free_out, fixed_out
+
+
+def fp64_best_solve(N, r, vals, mask, times):
+    """What a backward-stable FP64 solve reaches on this problem: R_pp and the right-hand side formed
+    exactly (60 digits) and rounded once to FP64, equilibrated (symmetric diagonal scaling), solved
+    by LU with partial pivoting (LAPACK via numpy), and mapped to coefficients with the correctly
+    rounded A(T)^-1 in FP64, positions taken relative to each segment's start (else the mapping alone
+    loses every digit of a millimetre segment far from the origin).  The arbiter for ill-conditioned problems (cond(R_pp) ~ 1e10 after
+    equilibration): no FP64 solver can be expected to beat it by much."""
+    h = N // 2
+    V, nd, D = vals.shape
+    K = V - 1
+    R, fixed, free, col, Ainvs, Qs = _system(N, r, vals, mask, times)
+    nf, npf = len(fixed), len(free)
+    coeffs = np.zeros((K, D, N))
+    Rf = np.array([[float(R[nf + a][nf + b]) for b in range(npf)] for a in range(npf)])
+    sc = 1.0 / np.sqrt(np.abs(np.diag(Rf))) if npf else np.zeros(0)
+    for d in range(D):
+        df = [mp.mpf(float(vals[v, k, d])) for (v, k) in fixed]
+        if npf:
+            rhs = np.array([float(-mp.fsum(R[nf + a][b] * df[b] for b in range(nf))) for a in range(npf)])
+            xp = np.linalg.solve(Rf * sc[:, None] * sc[None, :], rhs * sc) * sc
+        else:
+            xp = np.zeros(0)
+        dall = np.concatenate([np.array([float(x) for x in df]), xp])
+        for i in range(K):
+            cols = [col[(i + (s >= h), s % h)] for s in range(N)]
+            Ai = np.array([[float(Ainvs[i][a, b]) for b in range(N)] for a in range(N)])
+            x = dall[cols].copy()
+            p0 = x[0]
+            if r >= 1:  # positions relative to the segment start (A^-1 maps a constant to c_0 only)
+                x[0] -= p0
+                x[h] -= p0
+            coeffs[i, d] = Ai @ x
+            if r >= 1:
+                coeffs[i, d, 0] += p0
+    return coeffs
 
 
 def pack(problems):
