@@ -284,10 +284,6 @@ def main():
     ap.add_argument("--split", action="store_true", help="two-kernel path (assembly + block Cholesky)")
     ap.add_argument("--general-kernel", action="store_true",
                     help="force the general LDS-resident fused kernel (A/B against the default)")
-    ap.add_argument("--lane-kernel", action="store_true",
-                    help="the lane-per-chain kernel where it applies (A/B against the default)")
-    ap.add_argument("--ip-kernel", action="store_true",
-                    help="the interior-waypoint lane kernel where it applies (A/B against the default)")
     ap.add_argument("--dl-kernel", action="store_true",
                     help="the dimension-lane kernel where it applies (A/B against the default)")
     ap.add_argument("--column-kernel", action="store_true",
@@ -355,13 +351,11 @@ def main():
     else:
         out_d = torch.empty((B, K, D, N), dtype=torch.float64, device=dev)
         # one step = one launch of the solve on torch's current stream
-        kw = dict(split=args.split, general=args.general_kernel, lane=args.lane_kernel, ip=args.ip_kernel, dl=args.dl_kernel,
-                  column=args.column_kernel)
+        kw = dict(split=args.split, general=args.general_kernel, dl=args.dl_kernel, column=args.column_kernel)
         step = ctx.solve_call(N, r, v_d, m_d, t_d, out_d, **kw)
         step_t = ctx_t.solve_call(N, r, v_d, m_d, t_d, out_d, **kw)
         nat = mtg._native
         kflags = ((nat.MTG_FLAG_SPLIT_KERNELS if args.split else 0) | (nat.MTG_FLAG_GENERAL_KERNEL if args.general_kernel else 0)
-                  | (nat.MTG_FLAG_LANE_KERNEL if args.lane_kernel else 0) | (nat.MTG_FLAG_IP_KERNEL if args.ip_kernel else 0)
                   | (nat.MTG_FLAG_DL_KERNEL if args.dl_kernel else 0) | (nat.MTG_FLAG_COLUMN_KERNEL if args.column_kernel else 0))
         kname = mtg._native.solve_kernel(N, D, K, r, kflags, B=B)
     stride = args.timing_stride

@@ -74,15 +74,8 @@ extern "C" {
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
 #define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
                                           (default: see mtg_solve_kernel) */
-#define MTG_FLAG_LANE_KERNEL 16u       /* the lane-per-chain kernel where it applies (N in {6, 8} with
-                                          K <= 12, N = 10 with K <= 10; D <= 4; a fifth of the default kernel's
-                                          instructions per trajectory, but latency-bound at one wave
-                                          per SIMD: DESIGN.md 3.2) */
-
-#define MTG_FLAG_IP_KERNEL 32u         /* the interior-waypoint lane kernel where it applies (N in {6, 8, 10, 12},
-                                          D <= 4, K in {4, 8, 10, 12}, r >= 1; waves whose masks are not
-                                          the reference generators' pattern run the column kernel inside
-                                          it): DESIGN.md 3.1b */
+/* (16u and 32u selected the lane-per-chain and interior-waypoint lane kernels, retired in round 4:
+ * measured slower than the default everywhere, DESIGN.md 3.2.  The bits are reserved and ignored.) */
 
 #define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10, K = 10, D <= 4, r >= 1;
                                           one lane per (chain, dimension), waves whose masks are not the
@@ -96,14 +89,10 @@ extern "C" {
                                           are one wave's latency) */
 
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
-#define MTG_KERNEL_LANE 1              /* one lane per elimination chain, 32 trajectories per wave
-                                          (MTG_FLAG_LANE_KERNEL) */
 #define MTG_KERNEL_COLUMN 2            /* default: register column kernel, a lane per column of G_v /
                                           per dimension, twisted (K <= 12, N = 12 up to K = 20) */
 #define MTG_KERNEL_GENERAL 3           /* general LDS-resident fused kernel (any K) */
 #define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
-#define MTG_KERNEL_IP 5                /* one lane per chain, interior-waypoint pattern, LDL^T factors kept
-                                          (MTG_FLAG_IP_KERNEL) */
 #define MTG_KERNEL_DL 6                /* one lane per (chain, dimension), interior-waypoint pattern
                                           (MTG_FLAG_DL_KERNEL) */
 

@@ -31,21 +31,17 @@ MTG_FLAG_DEVICE_PTRS = 1
 MTG_FLAG_ASYNC = 2
 MTG_FLAG_SPLIT_KERNELS = 4
 MTG_FLAG_GENERAL_KERNEL = 8
-MTG_FLAG_LANE_KERNEL = 16
-MTG_FLAG_IP_KERNEL = 32
 MTG_FLAG_DL_KERNEL = 64
 MTG_FLAG_COLUMN_KERNEL = 128
 MTG_DL_MIN_BATCH = 2048
 
-MTG_KERNEL_LANE = 1
 MTG_KERNEL_COLUMN = 2
 MTG_KERNEL_GENERAL = 3
 MTG_KERNEL_SPLIT = 4
-MTG_KERNEL_IP = 5
 MTG_KERNEL_DL = 6
-KERNEL_NAMES = {MTG_KERNEL_LANE: "solve_lane_kernel", MTG_KERNEL_COLUMN: "solve_reg_kernel",
+KERNEL_NAMES = {MTG_KERNEL_COLUMN: "solve_reg_kernel",
                 MTG_KERNEL_GENERAL: "solve_fused_kernel", MTG_KERNEL_SPLIT: "assemble+block_cholesky",
-                MTG_KERNEL_IP: "solve_ip_kernel", MTG_KERNEL_DL: "solve_dl_kernel"}
+                MTG_KERNEL_DL: "solve_dl_kernel"}
 
 _c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
 

@@ -483,7 +483,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 && !scales &&
       (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes) {
     // the chunks run the kernel the whole batch would (the default depends on the batch size)
-    const unsigned kf = flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL |
+    const unsigned kf = flags & (MTG_FLAG_GENERAL_KERNEL |
                                  MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
     const unsigned pin = mtg::solve_kernel(N, D, K, kf, r, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
                                                                                      : MTG_FLAG_COLUMN_KERNEL;
@@ -589,7 +589,7 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_LANE_KERNEL | MTG_FLAG_IP_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL)));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL)));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (pin) {

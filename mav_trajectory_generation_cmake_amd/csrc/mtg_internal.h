@@ -55,21 +55,15 @@ bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes,
 
 // Launch the fused solve on `stream` with the kernel solve_kernel() picks: the register column
 // kernel (mtg_solve_reg.hip) where reg_geometry allows it (K <= 12, or N = 12 with K <= 20), else
-// the general LDS-resident kernel (mtg_kernels.hip); MTG_FLAG_LANE_KERNEL selects the
-// lane-per-chain kernel (mtg_solve_lane.hip) where lane_geometry allows it, MTG_FLAG_GENERAL_KERNEL
-// the general kernel.
+// the general LDS-resident kernel (mtg_kernels.hip); the dimension-lane kernel (mtg_solve_dl.hip)
+// where dl_geometry allows it; MTG_FLAG_GENERAL_KERNEL the general kernel.
 // B: the batch (trajectories, or trajectory x candidate pairs; < 0: below MTG_DL_MIN_BATCH).
 int solve_kernel(int N, int D, int K, unsigned flags, int r = -1, int64_t B = -1);  // MTG_KERNEL_*
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags = 0);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);
 hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
-bool lane_geometry(int N, int D, int K, size_t* lds_bytes);
-hipError_t launch_solve_lane(int N, const SolveArgs& a, hipStream_t stream);
-// lane kernel of the interior-waypoint pattern (mtg_solve_ip.hip): ends fix every derivative,
-// interior vertices exactly their position; other waves run the column kernel's block function
-bool ip_geometry(int N, int D, int K, int r);
-hipError_t launch_solve_ip(int N, const SolveArgs& a, hipStream_t stream);
-// dimension-lane kernel of the same pattern (mtg_solve_dl.hip): one lane per (chain, dimension)
+// dimension-lane kernel of the interior-waypoint pattern (mtg_solve_dl.hip: ends fix every
+// derivative, interior vertices exactly their position): one lane per (chain, dimension)
 bool dl_geometry(int N, int D, int K, int r);
 hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream);
 

@@ -110,8 +110,6 @@ int solve_kernel(int N, int D, int K, unsigned flags, int r, int64_t B) {
   int lg;
   size_t lds;
   if (flags & MTG_FLAG_GENERAL_KERNEL) return MTG_KERNEL_GENERAL;
-  if ((flags & MTG_FLAG_LANE_KERNEL) && lane_geometry(N, D, K, &lds)) return MTG_KERNEL_LANE;
-  if ((flags & MTG_FLAG_IP_KERNEL) && r >= 0 && ip_geometry(N, D, K, r)) return MTG_KERNEL_IP;
   // the dimension-lane kernel: asked for, or by default for large batches (at
   // B = 125000 ~15% faster than the column kernel, at 1e4 within the box-to-box spread)
   const bool dl_default = B >= MTG_DL_MIN_BATCH && !(flags & MTG_FLAG_COLUMN_KERNEL);
@@ -122,8 +120,6 @@ int solve_kernel(int N, int D, int K, unsigned flags, int r, int64_t B) {
 
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags) {
   switch (solve_kernel(N, a.D, a.K, flags, a.r, a.B)) {
-    case MTG_KERNEL_LANE: return launch_solve_lane(N, a, stream);
-    case MTG_KERNEL_IP: return launch_solve_ip(N, a, stream);
     case MTG_KERNEL_DL: return launch_solve_dl(N, a, stream);
     case MTG_KERNEL_COLUMN: return launch_solve_reg(N, a, stream);
     default: break;

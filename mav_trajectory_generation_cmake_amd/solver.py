@@ -87,7 +87,7 @@ class Context:
         return np.array(buf[:got.value], dtype=np.float64)
 
     def solve_call(self, N, r, values, mask, times, coeffs, free=None, n_free=None, cost=None, status=None,
-                   split=False, general=False, lane=False, ip=False, dl=False, column=False):
+                   split=False, general=False, dl=False, column=False):
         """A zero-argument callable that launches one device-pointer solve asynchronously on the
         current stream with the arguments bound once (the bench's step; minimal host overhead)."""
         import torch
@@ -96,8 +96,6 @@ class Context:
         self.set_stream(torch.cuda.current_stream(values.device).cuda_stream)
         flags = nat.MTG_FLAG_DEVICE_PTRS | nat.MTG_FLAG_ASYNC | (nat.MTG_FLAG_SPLIT_KERNELS if split else 0)
         flags |= nat.MTG_FLAG_GENERAL_KERNEL if general else 0
-        flags |= nat.MTG_FLAG_LANE_KERNEL if lane else 0
-        flags |= nat.MTG_FLAG_IP_KERNEL if ip else 0
         flags |= nat.MTG_FLAG_DL_KERNEL if dl else 0
         flags |= nat.MTG_FLAG_COLUMN_KERNEL if column else 0
         fn = self._lib.mtg_solve_linear_batch
@@ -149,8 +147,8 @@ class Context:
 
     # ------------------------------------------------------------------ solve
     def solve_linear_batch(self, N, r, values, mask, times, coeffs=None, free=None, n_free=None,
-                           cost=None, status=None, split=False, asynchronous=False, general=False, lane=False,
-                           ip=False, dl=False, column=False):
+                           cost=None, status=None, split=False, asynchronous=False, general=False, dl=False,
+                           column=False):
         """Solve a batch; returns dict of outputs (allocates those not given).
 
         want-flags: pass arrays (or True to allocate) for free / n_free / cost / status."""
@@ -195,10 +193,6 @@ class Context:
             flags |= nat.MTG_FLAG_SPLIT_KERNELS
         if general:
             flags |= nat.MTG_FLAG_GENERAL_KERNEL
-        if lane:
-            flags |= nat.MTG_FLAG_LANE_KERNEL
-        if ip:
-            flags |= nat.MTG_FLAG_IP_KERNEL
         if dl:
             flags |= nat.MTG_FLAG_DL_KERNEL
         if column:
@@ -210,7 +204,7 @@ class Context:
         return out
 
     def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
-                         asynchronous=False, split=False, ip=False, dl=False, column=False):
+                         asynchronous=False, split=False, dl=False, column=False):
         dev = _is_torch(values) and values.is_cuda
         B, V, h, D = values.shape
         K = V - 1
@@ -230,8 +224,6 @@ class Context:
             self.reset_stream()
         if split:
             flags |= nat.MTG_FLAG_SPLIT_KERNELS
-        if ip:
-            flags |= nat.MTG_FLAG_IP_KERNEL
         if dl:
             flags |= nat.MTG_FLAG_DL_KERNEL
         if column:

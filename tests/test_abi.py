@@ -119,21 +119,25 @@ def test_cpp_header_compiles_with_c_compiler(tmp_path):
 
 def test_solve_kernel_selection():
     """mtg_solve_kernel (host-only query): the register column kernel by default for K <= 12 (N = 12:
-    K <= 20), the lane-per-chain kernel with MTG_FLAG_LANE_KERNEL where it applies, the general kernel
-    beyond, errors for rejected shapes."""
+    K <= 20), the dimension-lane kernel with MTG_FLAG_DL_KERNEL where it applies, the general kernel
+    beyond, errors for rejected shapes; the retired lane / IP flag bits (16, 32) are ignored."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     lib = nat.load()
-    lane, col, gen, split = (nat.MTG_KERNEL_LANE, nat.MTG_KERNEL_COLUMN, nat.MTG_KERNEL_GENERAL,
-                             nat.MTG_KERNEL_SPLIT)
-    L = nat.MTG_FLAG_LANE_KERNEL
+    dl, col, gen, split = (nat.MTG_KERNEL_DL, nat.MTG_KERNEL_COLUMN, nat.MTG_KERNEL_GENERAL,
+                           nat.MTG_KERNEL_SPLIT)
+    L = nat.MTG_FLAG_DL_KERNEL
     assert lib.mtg_solve_kernel(10, 3, 10, 4, 0) == col  # config 2 / 3
     assert lib.mtg_solve_kernel(12, 3, 20, 3, 0) == col  # config 4
     assert lib.mtg_solve_kernel(4, 3, 10, 1, 0) == col
-    assert lib.mtg_solve_kernel(10, 3, 10, 4, L) == lane
-    assert lib.mtg_solve_kernel(10, 3, 1, 4, L) == lane
-    assert lib.mtg_solve_kernel(8, 1, 12, 3, L) == lane
-    assert lib.mtg_solve_kernel(6, 3, 12, 2, L) == lane
-    assert lib.mtg_solve_kernel(10, 5, 10, 4, L) == col   # D > 4: no lane kernel
+    assert lib.mtg_solve_kernel(10, 3, 10, 4, L) == dl
+    assert lib.mtg_solve_kernel(10, 1, 10, 1, L) == dl
+    assert lib.mtg_solve_kernel(10, 4, 10, 3, L) == dl
+    assert lib.mtg_solve_kernel(10, 3, 1, 4, L) == col    # K != 10: no DL kernel
+    assert lib.mtg_solve_kernel(8, 1, 12, 3, L) == col
+    assert lib.mtg_solve_kernel(10, 5, 10, 4, L) == col   # D > 4: no DL kernel
+    assert lib.mtg_solve_kernel(10, 3, 10, 0, L) == col   # r = 0: no translation trick
+    for retired in (16, 32):
+        assert lib.mtg_solve_kernel(10, 3, 10, 4, retired) == col
     assert lib.mtg_solve_kernel(12, 3, 20, 3, L) == col
     assert lib.mtg_solve_kernel(10, 3, 12, 4, 0) == gen   # G of 6 vertices exceeds both register budgets
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
@@ -158,4 +162,4 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(11, 3, 10, 4, 0) == nat.MTG_ERR_UNSUPPORTED_N
     assert lib.mtg_solve_kernel(10, 3, 10, 5, 0) == nat.MTG_ERR_BAD_DERIVATIVE
     assert nat.solve_kernel(10, 3, 10, 4) == "solve_reg_kernel"
-    assert nat.solve_kernel(10, 3, 10, 4, L) == "solve_lane_kernel"
+    assert nat.solve_kernel(10, 3, 10, 4, L) == "solve_dl_kernel"

@@ -20,11 +20,11 @@ TRUTH_TOL = 1e-9
 ORACLE_TOL_N10 = 1e-6
 
 # the solve paths behind mtg_solve_linear_batch: the default (mtg_solve_kernel: the register column
-# kernel for K <= 12 and for N = 12 up to K = 20, else the general one), the lane-per-chain kernel
-# (MTG_FLAG_LANE_KERNEL, where it applies), the general LDS-resident fused kernel, and the two-kernel
-# split path
-PATHS = {"default": {}, "lane": {"lane": True}, "general": {"general": True}, "split": {"split": True},
-         "ip": {"ip": True}, "dl": {"dl": True}}
+# kernel for K <= 12 and for N = 12 up to K = 20, else the general one; the dimension-lane kernel for
+# the shapes it serves), the general LDS-resident fused kernel, the two-kernel split path, the
+# dimension-lane kernel asked for (MTG_FLAG_DL_KERNEL, where it applies) and the column kernel asked for
+PATHS = {"default": {}, "general": {"general": True}, "split": {"split": True}, "dl": {"dl": True},
+         "column": {"column": True}}
 
 
 def _oracle():
@@ -220,7 +220,7 @@ def test_paths_agree_mixed_masks(gpu_ctx):
     for p, o in outs.items():
         assert np.all(o["status"] == 0), p
         assert scale_normalised_error(o["coeffs"], ref, times) <= 1e-6, p
-    for p in ("lane", "general", "split", "ip", "dl"):
+    for p in ("general", "split", "dl", "column"):
         assert scale_normalised_error(outs[p]["coeffs"], outs["default"]["coeffs"], times) <= 1e-9, p
 
 
@@ -910,70 +910,12 @@ def test_evaluate_range_full_one_call(gpu_ctx, B):
             np.testing.assert_array_equal(got[0], ref[0])
 
 
-@pytest.mark.parametrize("N,K,D,r", [(10, 10, 3, 4), (10, 8, 2, 3), (8, 12, 3, 3), (6, 4, 1, 1), (12, 8, 4, 5),
-                                     (10, 4, 4, 2)])
-def test_ip_kernel_vs_column_and_oracle(gpu_ctx, N, K, D, r):
-    """The interior-waypoint lane kernel (MTG_FLAG_IP_KERNEL): the reference generators' pattern
-    against the column kernel (1e-9, scale-normalised) and the oracle; free values, n_free, cost and
-    status; a ragged last wave; waves whose masks break the pattern (one trajectory with an extra
-    fixed derivative) run the column kernel's block function inside it, bit-identical to it."""
-    from mav_trajectory_generation_cmake_amd import _native as nat
-    O = _oracle()
-    assert nat.solve_kernel(N, D, K, r, nat.MTG_FLAG_IP_KERNEL) == "solve_ip_kernel"
-    from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
-    B = 101
-    # the reference generator with the ends fixed up to N/2 - 1 (every derivative the solver keeps)
-    vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=77, max_derivative=N // 2 - 1)
-    kw = dict(status=True, cost=True, free=True, n_free=True)
-    ip = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, ip=True, **kw)
-    col = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
-    assert np.all(ip["status"] == 0)
-    np.testing.assert_array_equal(ip["n_free"], col["n_free"])
-    assert scale_normalised_error(ip["coeffs"], col["coeffs"], times) <= 1e-9
-    np.testing.assert_allclose(ip["cost"], col["cost"], rtol=1e-9)
-    fs = np.max(np.abs(col["free"]), axis=2, keepdims=True)
-    assert np.max(np.abs(ip["free"] - col["free"]) / fs) <= 1e-8
-    ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
-    assert scale_normalised_error(ip["coeffs"], ref, times) <= (1e-6 if N <= 10 else 1e-3)
-    assert check_path(vals, mask, times, ip["coeffs"], N, relative=True) < 1e-6
-    # a wave with another pattern: trajectory 40 (wave 1) fixes a velocity at vertex 2
-    m2 = mask.copy()
-    m2[40, 2] |= 2
-    ip2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, ip=True, **kw)
-    col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, **kw)
-    for k in ("coeffs", "cost", "free", "status"):
-        np.testing.assert_array_equal(ip2[k][32:64], col2[k][32:64], err_msg=k)
-        np.testing.assert_array_equal(ip2[k][:32], ip[k][:32], err_msg=k)
-
-
-def test_ip_kernel_time_sweep_and_status(gpu_ctx):
-    """The IP kernel under the time sweep (trajectory x candidate pairs, scaled times) equals the
-    column kernel's sweep; bad and tiny segment times set the same status bits."""
-    from mav_trajectory_generation_cmake_amd import _native as nat
-    vals, mask, times = _bench_batch(70, seed0=5)
-    scales = np.array([0.7, 1.0, 1.9])
-    a = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales, ip=True)
-    b = gpu_ctx.time_sweep_batch(10, 4, vals, mask, times, scales)
-    np.testing.assert_allclose(a, b, rtol=1e-9)
-    t = times.copy()
-    t[3, 2] = 0.0
-    t[4, 7] = 1e-17
-    t[5, :] = 1e200
-    o = gpu_ctx.solve_linear_batch(10, 4, vals, mask, t, status=True, ip=True)
-    assert o["status"][3] & nat.MTG_TRAJ_BAD_TIME
-    assert o["status"][4] & nat.MTG_TRAJ_NOT_SPD and not o["status"][4] & nat.MTG_TRAJ_BAD_TIME
-    assert o["status"][5] & nat.MTG_TRAJ_NOT_SPD
-    assert np.all(o["status"][6:] == 0) and np.all(o["status"][:3] == 0)
-
-
 @pytest.mark.parametrize("D,r", [(3, 4), (1, 4), (2, 3), (4, 4), (3, 3)])
-def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
+def test_dl_kernel_vs_column_and_oracle(gpu_ctx, D, r):
     """The dimension-lane kernel (MTG_FLAG_DL_KERNEL): the reference generators' pattern against the
-    IP kernel (same arithmetic per dimension; the compiler contracts products into FMAs differently in
-    the two kernels, which the conditioning of R_pp amplifies to ~3e-10: 1e-9), the column kernel
-    (1e-8, scale-normalised: the host path and the oracle differ by up to 1.4e-8 on these batches) and
-    the oracle; free values, n_free, cost and status; a ragged last wave; a wave whose masks break the
-    pattern runs the general kernel's block function inside it, bit-identical to it."""
+    column kernel (1e-8, scale-normalised: the host path and the oracle differ by up to 1.4e-8 on these
+    batches) and the oracle; free values, n_free, cost and status; a ragged last wave; a wave whose
+    masks break the pattern runs the general kernel's block function inside it, bit-identical to it."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
     O = _oracle()
@@ -988,11 +930,9 @@ def test_dl_kernel_vs_ip_column_and_oracle(gpu_ctx, D, r):
     times = np.maximum(times, 0.5)
     kw = dict(status=True, cost=True, free=True, n_free=True)
     dl = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, dl=True, **kw)
-    ip = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, ip=True, **kw)
-    col = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    col = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, column=True, **kw)
     assert np.all(dl["status"] == 0)
     np.testing.assert_array_equal(dl["n_free"], col["n_free"])
-    assert scale_normalised_error(dl["coeffs"], ip["coeffs"], times) <= 1e-9
     assert scale_normalised_error(dl["coeffs"], col["coeffs"], times) <= 1e-8
     np.testing.assert_allclose(dl["cost"], col["cost"], rtol=1e-9)
     fs = np.max(np.abs(col["free"]), axis=2, keepdims=True)
