@@ -31,18 +31,24 @@ typedef Eigen::VectorXd VectorXd;
 typedef Eigen::MatrixXd MatrixXd;
 template <int R, int C>
 using FixedMatrix = Eigen::Matrix<double, R, C>;
+// the allocator of containers of fixed-size matrices (polynomial_optimization_linear.h:53-54)
+template <typename T>
+using AlignedAllocator = Eigen::aligned_allocator<T>;
 }  // namespace mav_trajectory_generation
 
 #else
 #include <cmath>
 #include <cstddef>
 #include <cstdlib>
+#include <memory>
 #include <ostream>
 #include <vector>
 
 namespace mav_trajectory_generation {
 
 typedef std::ptrdiff_t Index;
+template <typename T>
+using AlignedAllocator = std::allocator<T>;  // (Eigen mode: Eigen::aligned_allocator)
 
 namespace detail {
 // sum of x_i * y_i in Eigen's reduction order for SSE2 packets of two doubles

@@ -96,7 +96,8 @@ class PolynomialOptimization {
   enum { N = _N };
   static constexpr int kHighestDerivativeToOptimize = N / 2 - 1;
   typedef FixedMatrix<N, N> SquareMatrix;
-  typedef std::vector<SquareMatrix> SquareMatrixVector;
+  // polynomial_optimization_linear.h:53-54: Eigen's aligned allocator (std::allocator without Eigen)
+  typedef std::vector<SquareMatrix, AlignedAllocator<SquareMatrix>> SquareMatrixVector;
 
   // lin_impl:33-44
   explicit PolynomialOptimization(size_t dimension)

@@ -160,6 +160,11 @@ int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D,
                                  const double* times, double* coeffs, double* free_out, int32_t* n_free_out,
                                  double* cost_out, int32_t* status, unsigned flags);
 
+/* Diagnostics: the next mtg_solve_linear_batch on ctx (also as one shard of a multi-device solve)
+ * returns `code` (a negative MTG_ERR_*) without touching any array, as a failing device would --
+ * for testing how a caller or mtg_solve_linear_batch_multi propagates a shard's failure. */
+int mtg_debug_fail_next_solve(mtg_ctx* ctx, int code);
+
 /* Batched Trajectory::evaluateRange (src/trajectory.cpp:68-128) over solved
  * trajectories, with the reference's sequential time accumulation (acc += dt)
  * reproduced exactly.  coeffs [B][K][D][N], times [B][K].  Sample counts are

@@ -67,6 +67,7 @@ _SIGNATURES = {
     "mtg_solve_linear_batch_multi": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                     ctypes.c_int, ctypes.c_int, ctypes.c_int64, _c_dp, _c_dp, _c_dp,
                                                     _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_uint]),
+    "mtg_debug_fail_next_solve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mtg_evaluate_range_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int64, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double,
                                                 ctypes.c_double, ctypes.c_int, _c_dp, _c_dp, _c_dp, _c_dp,

@@ -91,6 +91,7 @@ struct mtg_ctx {
   int64_t launches = 0;
   std::string last_error;
   std::mutex mu;
+  int inject_rc = 0;  // mtg_debug_fail_next_solve: the next solve's return code (0: none)
   // Pipelined host-pointer solves (run_solve_pipelined): kPipeSlots chunks in flight, each with its
   // own kernel stream and device buffers; all H2D copies go through one stream and all D2H copies
   // through another (one copy queue per direction).
@@ -738,8 +739,20 @@ int mtg_solve_linear_batch(mtg_ctx* ctx, int N, int D, int K, int derivative_to_
   if (!values || !fixed_mask || !times)
     return set_error(ctx, MTG_ERR_INVALID_ARGUMENT, "values, fixed_mask and times are required");
   std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->inject_rc) {  // (diagnostics: mtg_debug_fail_next_solve)
+    const int code = ctx->inject_rc;
+    ctx->inject_rc = 0;
+    return set_error(ctx, code, "injected fault (mtg_debug_fail_next_solve)");
+  }
   return run_solve(ctx, N, D, K, derivative_to_optimize, batch, values, fixed_mask, times, coeffs,
                    free_out, n_free_out, cost_out, status, 1, nullptr, flags);
+}
+
+int mtg_debug_fail_next_solve(mtg_ctx* ctx, int code) {
+  if (!ctx || code >= 0) return MTG_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->inject_rc = code;
+  return MTG_OK;
 }
 
 int mtg_shard_range(int64_t batch, int n_shards, int shard, int64_t* begin, int64_t* end) {
@@ -796,10 +809,13 @@ int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D,
   for (auto& t : pool) t.join();
   for (int g = 0; g < n_ctxs; ++g) {
     if (rcs[g] == MTG_OK) continue;
-    if (g > 0) {
-      std::lock_guard<std::mutex> l(c0->mu);
-      c0->last_error = "shard " + std::to_string(g) + ": " + ctxs[g]->last_error;
+    std::string what;
+    {
+      std::lock_guard<std::mutex> l(ctxs[g]->mu);
+      what = ctxs[g]->last_error;
     }
+    std::lock_guard<std::mutex> l(c0->mu);
+    c0->last_error = "shard " + std::to_string(g) + " of " + std::to_string(n_ctxs) + ": " + what;
     return rcs[g];
   }
   return MTG_OK;
@@ -1165,7 +1181,7 @@ int mtg_evaluate_range_batch_full(mtg_ctx* ctx, int N, int D, int K, int64_t bat
                                                   ctx->workspace, cap, total, ctx->stream));
     MTG_HIP_TRY(ctx, mtg::launch_eval_range(N, D, K, batch, coeffs, times, t_start, t_end, dt, derivative, counts,
                                             offsets, out, sample_times, ctx->workspace, cap, ctx->stream, true,
-                                            offsets, capacity));
+                                            offsets, capacity, total));
     MTG_HIP_TRY(ctx, time_end(ctx));
     if (flags & MTG_FLAG_ASYNC) return MTG_OK;
     int64_t tot = 0;
@@ -1223,6 +1239,7 @@ int mtg_evaluate_range_batch_full(mtg_ctx* ctx, int N, int D, int K, int64_t bat
                                             reinterpret_cast<const double*>(base + o_times), t_start, t_end, dt,
                                             derivative, d_cnt, d_offs, nullptr, nullptr, ctx->workspace, cap,
                                             ctx->stream, true, d_offs, 0));
+    MTG_HIP_TRY(ctx, time_end(ctx));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(counts, d_cnt, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
     MTG_HIP_TRY(ctx, hipMemcpyAsync(offsets, d_offs, b_cnt, hipMemcpyDeviceToHost, ctx->stream));
     MTG_HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

@@ -348,7 +348,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
                                                                   double* sample_times, int cap,
                                                                   const RunHead* heads, const RunRec* runs,
                                                                   const int64_t* boff, int64_t* offsets_out,
-                                                                  int64_t capacity) {
+                                                                  int64_t capacity, const int64_t* total) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
   // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
 #pragma clang fp contract(off)
@@ -359,7 +359,9 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
   // offsets: given (offsets[b]), or device-side (the in-block prefix offsets[b] + the block's offset)
   const int64_t base = boff ? offsets[b] + boff[b >> 6] : offsets[b];
   if (boff && lane == 0) offsets_out[b] = base;
-  if (n_total <= 0 || base + n_total > capacity) return;  // (past the caller's capacity: nothing written)
+  // (past the caller's capacity -- this trajectory's rows, or the call's total when it is known on the
+  // device: then nothing at all is written)
+  if (n_total <= 0 || base + n_total > capacity || (total && *total > capacity)) return;
   RunLds* rt = reinterpret_cast<RunLds*>(lds);
   double* cf = reinterpret_cast<double*>(rt + 1);  // [K][D][N]
   double* ob = cf + K * D * N;                     // [kEvalThreads][D] output block
@@ -634,7 +636,8 @@ hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs, const double* times,
                              double t_start, double t_end, double dt, int derivative, const int64_t* counts,
                              const int64_t* offsets, double* out, double* sample_times, void* ws, int cap,
-                             hipStream_t stream, bool runs_ready, int64_t* offsets_out, int64_t capacity) {
+                             hipStream_t stream, bool runs_ready, int64_t* offsets_out, int64_t capacity,
+                             const int64_t* total) {
   if (B == 0) return hipSuccess;
   RunHead* heads = nullptr;
   RunRec* runs = nullptr;
@@ -663,11 +666,11 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
     if (d3)                                                                                                        \
       launch_kernel(eval_range_kernel<NN, DER, 3>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
                     t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
-                    offsets_out, capacity);                                                                        \
+                    offsets_out, capacity, total);                                                                 \
     else                                                                                                           \
       launch_kernel(eval_range_kernel<NN, DER, 0>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
                     t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
-                    offsets_out, capacity);                                                                        \
+                    offsets_out, capacity, total);                                                                 \
   } while (0)
 #define MTG_EVAL_CASE(NN)                 \
   case NN:                                \

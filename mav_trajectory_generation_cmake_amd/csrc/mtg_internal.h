@@ -103,12 +103,13 @@ size_t eval_workspace_bytes(int K, int64_t B, int* cap);
 // (eval_runs_kernel); with runs_ready, launch_eval_runs_counts already built it together with the
 // counts and the two-level offsets: offsets then holds the in-block prefix and the kernel writes the
 // final offsets to offsets_out.  A trajectory whose samples would end past `capacity` samples is
-// not written.
+// not written, and none is when the device-side `total` (nullable) exceeds it.
 hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeffs,
                              const double* times, double t_start, double t_end, double dt,
                              int derivative, const int64_t* counts, const int64_t* offsets, double* out,
                              double* sample_times, void* ws, int cap, hipStream_t stream, bool runs_ready = false,
-                             int64_t* offsets_out = nullptr, int64_t capacity = INT64_MAX);
+                             int64_t* offsets_out = nullptr, int64_t capacity = INT64_MAX,
+                             const int64_t* total = nullptr);
 // The one-call evaluateRange's first two kernels: the run table plus counts[B] and the in-block
 // offsets (eval_runs_kernel), then the block offsets and the grand total (eval_scan_kernel); all
 // device-side, no host round trip.  Workspace: eval_full_workspace_bytes.

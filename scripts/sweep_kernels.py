@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel time (HIP events in the dispatch packet, mean of 64 launches after 64 warmups) of the
-config-2 solve vs batch size, for the kernels named in KERNELS (lane, column, ip, dl), in one process.
+config-2 solve vs batch size, for the kernels named in KERNELS (column, dl, default, general), in one process.
 
 Run on the GPU box: python scripts/sweep_kernels.py [B ...]"""
 import os
@@ -20,9 +20,8 @@ out = torch.empty((max(Bs), 10, 3, 10), dtype=torch.float64, device=dev)
 ctx = mtg.Context(0)
 for B in Bs:
     row = {"B": B}
-    kinds = (("lane", {"lane": True}), ("column", {"column": True}), ("ip", {"ip": True}), ("dl", {"dl": True}),
-             ("default", {}))
-    for name, kw in [k for k in kinds if k[0] in os.environ.get("KERNELS", "lane,column").split(",")]:
+    kinds = (("column", {"column": True}), ("dl", {"dl": True}), ("default", {}), ("general", {"general": True}))
+    for name, kw in [k for k in kinds if k[0] in os.environ.get("KERNELS", "column,dl").split(",")]:
         step = ctx.solve_call(10, 4, v_d[:B], m_d[:B], t_d[:B], out[:B], **kw)
         ctx.enable_timing(0)
         for _ in range(64):

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <random>
+#include <type_traits>
 #include <vector>
 
 #include <eigen3/Eigen/Core>
@@ -165,6 +166,18 @@ static void two_vertices_setup() {
   mtg::PolynomialOptimization<10>::invertMappingMatrix(A, &A_inv);
   const Eigen::MatrixXd I = A_inv * A;
   EXPECT((I - Eigen::MatrixXd::Identity(10, 10)).cwiseAbs().maxCoeff() < 1e-10 * std::pow(5.0, 9), "A^-1 A");
+  // the container type spelled out as the reference declares it (polynomial_optimization_linear.h:53-54)
+  typedef mtg::PolynomialOptimization<10>::SquareMatrix SM;
+  static_assert(std::is_same<mtg::PolynomialOptimization<10>::SquareMatrixVector,
+                             std::vector<SM, Eigen::aligned_allocator<SM>>>::value,
+                "SquareMatrixVector is std::vector<SquareMatrix, Eigen::aligned_allocator<SquareMatrix>>");
+  std::vector<SM, Eigen::aligned_allocator<SM>> inverses(3);
+  for (int i = 0; i < 3; ++i) {
+    mtg::PolynomialOptimization<10>::setupMappingMatrix(1.0 + i, &A);
+    mtg::PolynomialOptimization<10>::invertMappingMatrix(A, &inverses[i]);
+  }
+  mtg::PolynomialOptimization<10>::SquareMatrixVector same = inverses;
+  EXPECT(same.size() == 3 && (same[2] - inverses[2]).cwiseAbs().maxCoeff() == 0.0, "SquareMatrixVector copy");
 }
 
 int main() {

@@ -805,6 +805,51 @@ def test_solve_linear_batch_multi_bitwise(gpu_ctx, B, n_ctx):
         np.testing.assert_array_equal(multi[k], one[k], err_msg=k)
 
 
+@pytest.mark.parametrize("fail", [0, 2])
+def test_solve_linear_batch_multi_shard_failure(gpu_ctx, fail):
+    """A failing shard of mtg_solve_linear_batch_multi (the failure injected with
+    mtg_debug_fail_next_solve, as a device that fails would): the call returns that shard's code,
+    mtg_last_error(ctxs[0]) names the shard, the failing shard's slice of every output is untouched, and
+    the other shards' slices hold exactly what one call over the whole batch gives.  (Contexts need a
+    device, so this runs on the GPU box: three contexts on device 0, the same code path as one per
+    device.)"""
+    import ctypes
+    import mav_trajectory_generation_cmake_amd as mtg
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd.solver import _addr
+    B, n_ctx = 3001, 3
+    vals, mask, times = _bench_batch(B, seed0=9100)
+    ctxs = [gpu_ctx] + [mtg.Context(0) for _ in range(n_ctx - 1)]
+    try:
+        lib = nat.load()
+        nat.check(lib.mtg_debug_fail_next_solve(ctxs[fail].handle, nat.MTG_ERR_OUT_OF_MEMORY))
+        coeffs = np.full((B, 10, 3, 10), 7.25)
+        cost = np.full(B, 7.25)
+        status = np.full(B, 77, np.int32)
+        handles = (ctypes.c_void_p * n_ctx)(*[c.handle for c in ctxs])
+        rc = lib.mtg_solve_linear_batch_multi(ctypes.cast(handles, ctypes.c_void_p), n_ctx, 10, 3, 10, 4, B,
+                                              _addr(vals), _addr(mask), _addr(times), _addr(coeffs), None, None,
+                                              _addr(cost), _addr(status), 0)
+        assert rc == nat.MTG_ERR_OUT_OF_MEMORY
+        msg = lib.mtg_last_error(ctxs[0].handle).decode()
+        assert msg.startswith("shard %d of %d" % (fail, n_ctx)) and "injected fault" in msg, msg
+        one = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times, cost=True, status=True)
+        for g in range(n_ctx):
+            b0, b1 = mtg.shard_range(B, n_ctx, g)
+            if g == fail:
+                assert np.all(coeffs[b0:b1] == 7.25) and np.all(cost[b0:b1] == 7.25) and np.all(status[b0:b1] == 77)
+            else:
+                np.testing.assert_array_equal(coeffs[b0:b1], one["coeffs"][b0:b1])
+                np.testing.assert_array_equal(cost[b0:b1], one["cost"][b0:b1])
+                np.testing.assert_array_equal(status[b0:b1], one["status"][b0:b1])
+        # the injection is one-shot: the same call now succeeds
+        again = mtg.solve_linear_batch_multi(ctxs, 10, 4, vals, mask, times)
+        np.testing.assert_array_equal(again["coeffs"], one["coeffs"])
+    finally:
+        for c in ctxs[1:]:
+            c.close()
+
+
 @pytest.mark.parametrize("K", [3, 10, 100, 200])
 def test_min_max_magnitude_gpu_matches_host(gpu_ctx, K):
     """The extrema kernel (8 / 8 / 4 / 2 lanes per segment for K = 3 / 10 / 100 / 200) and the host
@@ -908,6 +953,19 @@ def test_evaluate_range_full_one_call(gpu_ctx, B):
             np.testing.assert_array_equal(offs, ref[3])
             got = gpu_ctx.evaluate_range_batch_full(coeffs, times, ts, te, dt, der, capacity=total - 1)
             np.testing.assert_array_equal(got[0], ref[0])
+            # device pointers: the same error, and not one sample row written (the kernel reads the
+            # device-side total), although most trajectories' rows would fit the short capacity
+            cnt_d = torch.empty(B, dtype=torch.int64, device="cuda")
+            off_d = torch.empty(B, dtype=torch.int64, device="cuda")
+            tot_d = torch.zeros(1, dtype=torch.int64, device="cuda")
+            out_d = torch.full((total - 1, 3), 7.25, dtype=torch.float64, device="cuda")
+            rc = gpu_ctx._lib.mtg_evaluate_range_batch_full(gpu_ctx.handle, 10, 3, 10, B, _addr(c_d), _addr(t_d), ts,
+                                                            te, dt, der, _addr(cnt_d), _addr(off_d), _addr(tot_d),
+                                                            _addr(out_d), None, total - 1, nat.MTG_FLAG_DEVICE_PTRS)
+            torch.cuda.synchronize()
+            assert rc == nat.MTG_ERR_TOO_LARGE and int(tot_d.item()) == total
+            assert bool((out_d == 7.25).all())
+            np.testing.assert_array_equal(cnt_d.cpu().numpy(), ref[2])
 
 
 @pytest.mark.parametrize("D,r", [(3, 4), (1, 4), (2, 3), (4, 4), (3, 3)])
