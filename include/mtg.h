@@ -78,15 +78,17 @@ extern "C" {
  * measured slower than the default everywhere, DESIGN.md 3.2.  The bits are reserved and ignored.) */
 
 #define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10, K = 10, D <= 4, r >= 1;
-                                          one lane per (chain, dimension), waves whose masks are not the
-                                          reference generators' pattern run the column kernel inside it):
-                                          DESIGN.md 3.2c.  The default for those shapes from
-                                          MTG_DL_MIN_BATCH trajectories on (mtg_solve_kernel_batch) */
+                                          one lane per (chain, dimension); trajectories whose masks are not
+                                          the reference generators' pattern are solved by the general fused
+                                          kernel's block function inside it, with the general kernel's
+                                          bits): DESIGN.md 3.2c.  The default for those shapes at every
+                                          batch size */
 #define MTG_FLAG_COLUMN_KERNEL 128u    /* the register column kernel wherever it applies, also where the
                                           default for the batch size is the dimension-lane kernel (A/B) */
-#define MTG_DL_MIN_BATCH 2048          /* batches from this size on run the dimension-lane kernel by default
-                                          where it applies (measured faster from 2048 on; below, both kernels
-                                          are one wave's latency) */
+#define MTG_DL_MIN_BATCH 1             /* (round 3: 2048.)  Since round 4 the dimension-lane kernel is the
+                                          default at every batch size where it applies, so a trajectory's
+                                          result never depends on the size of the call or on the other
+                                          trajectories in it (it was faster at every size) */
 
 /* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
 #define MTG_KERNEL_COLUMN 2            /* default: register column kernel, a lane per column of G_v /
@@ -103,8 +105,8 @@ int mtg_abi_version(void);
 /* The solve kernel (MTG_KERNEL_*) mtg_solve_linear_batch runs for this shape and these flags, or a
    negative MTG_ERR_* for a shape it rejects.  No device work. */
 int mtg_solve_kernel(int N, int D, int K, int derivative_to_optimize, unsigned flags);
-/* The same for a batch of B trajectories (or trajectory x candidate pairs): the default kernel depends
-   on B (MTG_DL_MIN_BATCH); mtg_solve_kernel answers for batches below MTG_DL_MIN_BATCH. */
+/* The same for a batch of B trajectories (or trajectory x candidate pairs).  Since round 4 the answer
+   does not depend on B (kept for round-3 callers). */
 int mtg_solve_kernel_batch(int N, int D, int K, int derivative_to_optimize, int64_t B, unsigned flags);
 const char* mtg_status_string(int code);
 const char* mtg_last_error(mtg_ctx* ctx);

@@ -33,7 +33,7 @@ MTG_FLAG_SPLIT_KERNELS = 4
 MTG_FLAG_GENERAL_KERNEL = 8
 MTG_FLAG_DL_KERNEL = 64
 MTG_FLAG_COLUMN_KERNEL = 128
-MTG_DL_MIN_BATCH = 2048
+MTG_DL_MIN_BATCH = 1
 
 MTG_KERNEL_COLUMN = 2
 MTG_KERNEL_GENERAL = 3

@@ -57,7 +57,8 @@ bool solve_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes,
 // kernel (mtg_solve_reg.hip) where reg_geometry allows it (K <= 12, or N = 12 with K <= 20), else
 // the general LDS-resident kernel (mtg_kernels.hip); the dimension-lane kernel (mtg_solve_dl.hip)
 // where dl_geometry allows it; MTG_FLAG_GENERAL_KERNEL the general kernel.
-// B: the batch (trajectories, or trajectory x candidate pairs; < 0: below MTG_DL_MIN_BATCH).
+// B: the batch (trajectories, or trajectory x candidate pairs; < 0: unknown).  The choice does not
+// depend on it (since round 4: the DL kernel at every size where it applies).
 int solve_kernel(int N, int D, int K, unsigned flags, int r = -1, int64_t B = -1);  // MTG_KERNEL_*
 hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned flags = 0);
 bool reg_geometry(int N, int D, int K, int* lanes_per_traj, size_t* lds_bytes);

@@ -110,9 +110,10 @@ int solve_kernel(int N, int D, int K, unsigned flags, int r, int64_t B) {
   int lg;
   size_t lds;
   if (flags & MTG_FLAG_GENERAL_KERNEL) return MTG_KERNEL_GENERAL;
-  // the dimension-lane kernel: asked for, or by default for large batches (at
-  // B = 125000 ~15% faster than the column kernel, at 1e4 within the box-to-box spread)
-  const bool dl_default = B >= MTG_DL_MIN_BATCH && !(flags & MTG_FLAG_COLUMN_KERNEL);
+  // the dimension-lane kernel wherever it applies, at every batch size, so that a
+  // trajectory's result does not depend on the size of the call it is in; MTG_FLAG_COLUMN_KERNEL
+  // keeps the column kernel (A/B)
+  const bool dl_default = !(flags & MTG_FLAG_COLUMN_KERNEL);
   if (((flags & MTG_FLAG_DL_KERNEL) || dl_default) && r >= 0 && dl_geometry(N, D, K, r)) return MTG_KERNEL_DL;
   if (reg_geometry(N, D, K, &lg, &lds)) return MTG_KERNEL_COLUMN;
   return MTG_KERNEL_GENERAL;

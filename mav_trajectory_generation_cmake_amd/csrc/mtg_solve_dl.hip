@@ -1,12 +1,10 @@
 // mtg_solve_dl.hip -- dispatch of the dimension-lane kernel (mtg_solve_dl.inc; one translation unit
 // per (N, D) in mtg_solve_dl_n*_d*.hip).
-#include <stdlib.h>
-
 #include "mtg_solve_dl.inc"  // (templates only: no kernel is instantiated in this unit)
 
 namespace mtg {
 
-#define MTG_DL_DECL(NN, DD) hipError_t launch_solve_dl_n##NN##_d##DD(const SolveArgs&, int, hipStream_t);
+#define MTG_DL_DECL(NN, DD) hipError_t launch_solve_dl_n##NN##_d##DD(const SolveArgs&, hipStream_t);
 MTG_DL_DECL(10, 1) MTG_DL_DECL(10, 2) MTG_DL_DECL(10, 3) MTG_DL_DECL(10, 4)
 #undef MTG_DL_DECL
 
@@ -19,21 +17,10 @@ bool dl_geometry(int N, int D, int K, int r) {
   return sizeof(double) * (size_t)dl_lds_doubles(N, D, K) <= kMaxLdsPerBlock && fb <= kMaxLdsPerBlock;
 }
 
-// Trajectories per wave: all 64 / (2 D) the lanes hold, unless MTG_DL_TPW asks for fewer (A/B).
-static int dl_tpw(int D) {
-  static const int env = [] {
-    const char* p = getenv("MTG_DL_TPW");
-    return p ? atoi(p) : 0;
-  }();
-  const int full = kBlock / (2 * D);
-  return env >= 1 && env < full ? env : full;
-}
-
 hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream) {
   if (!dl_geometry(N, a.D, a.K, a.r)) return hipErrorInvalidValue;
-  const int tpw = dl_tpw(a.D);
 #define MTG_DL_CASE(NN, DD) \
-  if (N == NN && a.D == DD) return launch_solve_dl_n##NN##_d##DD(a, tpw, stream);
+  if (N == NN && a.D == DD) return launch_solve_dl_n##NN##_d##DD(a, stream);
   MTG_DL_CASE(10, 1) MTG_DL_CASE(10, 2) MTG_DL_CASE(10, 3) MTG_DL_CASE(10, 4)
 #undef MTG_DL_CASE
   return hipErrorInvalidValue;

@@ -29,9 +29,20 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--contexts", default="1,8")
     args = ap.parse_args()
+    import ctypes
     import torch
     import bench
     import mav_trajectory_generation_cmake_amd as mtg
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd.solver import _addr
+    lib = nat.load()
+
+    def multi(ctxs, v, m, t, out):
+        # outputs preallocated and touched once (a fresh array per call would measure page faults)
+        handles = (ctypes.c_void_p * len(ctxs))(*[c.handle for c in ctxs])
+        nat.check(lib.mtg_solve_linear_batch_multi(ctypes.cast(handles, ctypes.c_void_p), len(ctxs), 10, 3, 10, 4,
+                                                   len(v), _addr(v), _addr(m), _addr(t), _addr(out), None, None,
+                                                   None, None, 0), ctxs[0].handle)
     host = bench.host_cpu_info()
     S = args.per_ctx
     v1, m1, t1 = mtg.random_vertices_path_batch(10, 3, 10, S, seed0=0)
@@ -45,13 +56,15 @@ def main():
             for mode in ("pageable", "pinned"):
                 if mode == "pinned":
                     v, m, t = (torch.from_numpy(x).pin_memory().numpy() for x in (vals, mask, times))
+                    out = torch.zeros((B, 10, 3, 10), dtype=torch.float64).pin_memory().numpy()
                 else:
                     v, m, t = vals, mask, times
-                mtg.solve_linear_batch_multi(ctxs, 10, 4, v, m, t)  # warm: buffers, threads
+                    out = np.zeros((B, 10, 3, 10))
+                multi(ctxs, v, m, t, out)  # warm: buffers, threads
                 walls, cpus = [], []
                 for _ in range(args.reps):
                     c0, w0 = time.process_time(), time.perf_counter()
-                    mtg.solve_linear_batch_multi(ctxs, 10, 4, v, m, t)
+                    multi(ctxs, v, m, t, out)
                     walls.append(time.perf_counter() - w0)
                     cpus.append(time.process_time() - c0)
                 wall, cpu = float(np.median(walls)), float(np.median(cpus))

@@ -126,7 +126,7 @@ def test_solve_kernel_selection():
     dl, col, gen, split = (nat.MTG_KERNEL_DL, nat.MTG_KERNEL_COLUMN, nat.MTG_KERNEL_GENERAL,
                            nat.MTG_KERNEL_SPLIT)
     L = nat.MTG_FLAG_DL_KERNEL
-    assert lib.mtg_solve_kernel(10, 3, 10, 4, 0) == col  # config 2 / 3
+    assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_COLUMN_KERNEL) == col  # config 2 / 3, column A/B
     assert lib.mtg_solve_kernel(12, 3, 20, 3, 0) == col  # config 4
     assert lib.mtg_solve_kernel(4, 3, 10, 1, 0) == col
     assert lib.mtg_solve_kernel(10, 3, 10, 4, L) == dl
@@ -137,20 +137,19 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(10, 5, 10, 4, L) == col   # D > 4: no DL kernel
     assert lib.mtg_solve_kernel(10, 3, 10, 0, L) == col   # r = 0: no translation trick
     for retired in (16, 32):
-        assert lib.mtg_solve_kernel(10, 3, 10, 4, retired) == col
+        assert lib.mtg_solve_kernel(10, 3, 10, 4, retired) == nat.MTG_KERNEL_DL
     assert lib.mtg_solve_kernel(12, 3, 20, 3, L) == col
     assert lib.mtg_solve_kernel(10, 3, 12, 4, 0) == gen   # G of 6 vertices exceeds both register budgets
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_SPLIT_KERNELS) == split
     assert lib.mtg_solve_kernel(10, 3, 13, 4, 0) == gen
-    # the batch-size-aware query: the dimension-lane kernel by default from MTG_DL_MIN_BATCH on, where
-    # it applies (N = 10, K = 10, D <= 4, r >= 1); the column flag keeps the column kernel
+    # the dimension-lane kernel by default wherever it applies (N = 10, K = 10, D <= 4, r >= 1), at
+    # every batch size (a trajectory's bits do not depend on the size of its call); the column flag
+    # keeps the column kernel
     dl = nat.MTG_KERNEL_DL
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 1024, 0) == col
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 8192, 0) == dl
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10000, 0) == dl  # config 2
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH - 1, 0) == col
-    assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, nat.MTG_DL_MIN_BATCH, 0) == dl
+    assert lib.mtg_solve_kernel(10, 3, 10, 4, 0) == dl
+    for B in (1, 10, 1024, 2047, 2048, 8192, 10000):
+        assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, B, 0) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 125000, nat.MTG_FLAG_COLUMN_KERNEL) == col
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10, nat.MTG_FLAG_DL_KERNEL) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 0, 125000, 0) == col  # r = 0: no translation trick
@@ -161,5 +160,5 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(10, 3, 50, 4, 0) == gen
     assert lib.mtg_solve_kernel(11, 3, 10, 4, 0) == nat.MTG_ERR_UNSUPPORTED_N
     assert lib.mtg_solve_kernel(10, 3, 10, 5, 0) == nat.MTG_ERR_BAD_DERIVATIVE
-    assert nat.solve_kernel(10, 3, 10, 4) == "solve_reg_kernel"
+    assert nat.solve_kernel(10, 3, 10, 4) == "solve_dl_kernel"
     assert nat.solve_kernel(10, 3, 10, 4, L) == "solve_dl_kernel"

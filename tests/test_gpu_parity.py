@@ -539,7 +539,7 @@ def test_g_in_lds_and_register_paths_bitwise_equal(gpu_ctx):
     dev = torch.device("cuda", 0)
     v_d, m_d, t_d = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (vals, mask, times))
     c_d = torch.empty((big, 10, 3, 10), dtype=torch.float64, device=dev)
-    # (the column kernel at both sizes: from MTG_DL_MIN_BATCH on the default is the DL kernel)
+    # (the column kernel at both sizes: the default for this shape is the DL kernel)
     gpu_ctx.solve_call(10, 4, v_d, m_d, t_d, c_d, column=True)()
     torch.cuda.synchronize()
     whole = c_d.cpu().numpy()
@@ -1048,8 +1048,7 @@ def test_dl_kernel_time_sweep_status_and_device_outputs(gpu_ctx):
 
 
 def test_time_sweep_large_default_runs_dl(gpu_ctx):
-    """A time sweep of 200 trajectories x 64 candidates (12800 pairs: the DL kernel by default, from
-    MTG_DL_MIN_BATCH on) equals the column kernel's sweep (rtol 1e-9) and re-solves at scaled times."""
+    """A time sweep of 200 trajectories x 64 candidates (12800 pairs: the DL kernel by default) equals the column kernel's sweep (rtol 1e-9) and re-solves at scaled times."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     assert nat.solve_kernel(10, 3, 10, 4, B=200 * 64) == "solve_dl_kernel"
     vals, mask, times = _bench_batch(200, seed0=61)
@@ -1064,7 +1063,7 @@ def test_time_sweep_large_default_runs_dl(gpu_ctx):
 
 @pytest.mark.parametrize("D", [1, 2, 4])
 def test_dl_default_path_other_dimensions_unclamped(gpu_ctx, D):
-    """The DL kernel is the default from MTG_DL_MIN_BATCH trajectories for N = 10, K = 10, D <= 4.
+    """The DL kernel is the default for N = 10, K = 10, D <= 4.
     D = 1, 2, 4 at B = 4096 on the DEFAULT path with the bench generator's own times (no clamp: the
     millisecond segments that make R_pp ill-conditioned stay in): the whole batch against the oracle
     and the relative checkPath on every trajectory (test/test_polynomial_optimization.cpp:73-131;
@@ -1117,3 +1116,38 @@ def test_dl_default_path_other_dimensions_unclamped(gpu_ctx, D):
     ok = errs <= ORACLE_TOL_N10
     assert np.mean(ok) >= 0.98
     np.testing.assert_allclose(out["cost"][ok], cost[ok], rtol=1e-6)
+
+
+@pytest.mark.parametrize("N,D,K,r", [(10, 3, 10, 4), (10, 1, 10, 2), (12, 3, 20, 3), (8, 2, 6, 2), (10, 3, 13, 4)])
+def test_result_independent_of_batch_composition(gpu_ctx, N, D, K, r):
+    """A trajectory's bits do not depend on the call it is in (the default kernel used to
+    change with the batch size, and a DL wave with one trajectory of another pattern sent all its
+    wave-mates through the general kernel).  Default path, a batch of 2500 with ~8% of trajectories
+    carrying extra fixed interior derivatives (another pattern): the whole batch, the batch reversed,
+    chunks of 37 and of 1500, and single trajectories all give the same coefficients, free values,
+    cost and status, bit for bit.  Shapes: config 2 and D = 1 (DL kernel), config 4 (wide column
+    bucket), N = 8 (column kernel), K = 13 (general kernel)."""
+    from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
+    B = 2500
+    vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=7700, max_derivative=min(4, N // 2 - 1))
+    rng = np.random.default_rng(5)
+    odd = rng.random(B) < 0.08
+    for b in np.nonzero(odd)[0]:
+        v = 1 + int(rng.integers(0, K - 1))
+        mask[b, v] |= np.uint8(2)  # the velocity fixed at one interior vertex (its value is in vals)
+    kw = dict(free=True, cost=True, status=True)
+    whole = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    assert np.all(whole["status"] == 0)
+    keys = ("coeffs", "free", "cost", "status")
+    rev = gpu_ctx.solve_linear_batch(N, r, vals[::-1].copy(), mask[::-1].copy(), times[::-1].copy(), **kw)
+    for k in keys:
+        np.testing.assert_array_equal(rev[k][::-1], whole[k], err_msg="reversed " + k)
+    for chunk in (37, 1500):
+        for s0 in range(0, B, chunk):
+            part = gpu_ctx.solve_linear_batch(N, r, vals[s0:s0 + chunk], mask[s0:s0 + chunk], times[s0:s0 + chunk], **kw)
+            for k in keys:
+                np.testing.assert_array_equal(part[k], whole[k][s0:s0 + chunk], err_msg="chunk %d %s" % (chunk, k))
+    for b in list(np.nonzero(odd)[0][:3]) + [0, 1, B - 1]:
+        one = gpu_ctx.solve_linear_batch(N, r, vals[b:b + 1], mask[b:b + 1], times[b:b + 1], **kw)
+        for k in keys:
+            np.testing.assert_array_equal(one[k], whole[k][b:b + 1], err_msg="single %d %s" % (b, k))
