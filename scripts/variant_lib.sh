@@ -2,6 +2,8 @@
 # dispatch (extra compile definitions or an edited mtg_solve_reg.inc), linked against the main
 # build's other objects (run `cmake --build build` first).  Timing A/B of N = 10 only: the other
 # N units keep the main build's code.  usage: bash scripts/variant_lib.sh NAME [-DMACRO[=V] ...]
+# UNITS: the units to rebuild; SRCDIR: where they (and the .inc they include) are taken from
+# (default csrc; e.g. a directory with an older mtg_solve_dl.inc checked out of git).
 # Output: mav_trajectory_generation_cmake_amd/lib_var/NAME/libmav_trajectory_generation.so
 set -e
 cd "$(dirname "$0")/.."
@@ -14,7 +16,7 @@ UNITS=${UNITS:-mtg_solve_reg_n10 mtg_solve_reg}  # (another kernel: UNITS="mtg_j
 for u in $UNITS; do
   /opt/rocm/llvm/bin/clang++ -D__HIP_ROCclr__=1 -Dmav_trajectory_generation_EXPORTS -I include \
     -I mav_trajectory_generation_cmake_amd/csrc -O3 -DNDEBUG -std=gnu++17 --offload-arch=gfx950 -fPIC \
-    -Wall -Wno-unused-parameter "$@" -o $OUT/$u.o -x hip -c mav_trajectory_generation_cmake_amd/csrc/$u.hip
+    -Wall -Wno-unused-parameter "$@" -o $OUT/$u.o -x hip -c ${SRCDIR:-mav_trajectory_generation_cmake_amd/csrc}/$u.hip
 done
 excl=""; for u in $UNITS; do excl="$excl -e /$u.hip.o\$"; done
 objs=$(ls $OBJ/*.o | grep -v $excl)
