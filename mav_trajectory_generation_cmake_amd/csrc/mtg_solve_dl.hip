@@ -6,15 +6,21 @@ namespace mtg {
 
 #define MTG_DL_DECL(NN, DD) hipError_t launch_solve_dl_n##NN##_d##DD(const SolveArgs&, hipStream_t);
 MTG_DL_DECL(10, 1) MTG_DL_DECL(10, 2) MTG_DL_DECL(10, 3) MTG_DL_DECL(10, 4)
+MTG_DL_DECL(12, 1) MTG_DL_DECL(12, 2) MTG_DL_DECL(12, 3) MTG_DL_DECL(12, 4)
 #undef MTG_DL_DECL
 
-// Shapes the kernel serves: N = 10, K = 10, D <= 4, r >= 1 (translation-relative positions), within
-// 64 KB of LDS for its own path and for the general kernel's block function (the waves of other
-// patterns).
+// Shapes the kernel serves: N = 10 with K = 10 (configs 2, 3) and N = 12 with K = 20 (config 4),
+// D <= 4, r >= 1 (translation-relative positions); its LDS (and the general kernel's block function's,
+// for the trajectories of other patterns) within a CU's 160 KB.
 bool dl_geometry(int N, int D, int K, int r) {
-  if (N != 10 || K != 10 || D < 1 || D > 4 || r < 1 || r > N / 2 - 1) return false;
-  const size_t fb = sizeof(double) * (size_t)kDlFallbackTraj * slot_doubles(N / 2, D, K, 1 << kDlFallbackLgLog2);
-  return sizeof(double) * (size_t)dl_lds_doubles(N, D, K) <= kMaxLdsPerBlock && fb <= kMaxLdsPerBlock;
+  if (D < 1 || D > 4 || r < 1 || r > N / 2 - 1 || K != dl_kmax(N) || K == 0) return false;
+  size_t lds = 0;
+#define MTG_DL_LDS(NN, DD) \
+  if (N == NN && D == DD) lds = dl_lds_bytes<NN, DD>();
+  MTG_DL_LDS(10, 1) MTG_DL_LDS(10, 2) MTG_DL_LDS(10, 3) MTG_DL_LDS(10, 4)
+  MTG_DL_LDS(12, 1) MTG_DL_LDS(12, 2) MTG_DL_LDS(12, 3) MTG_DL_LDS(12, 4)
+#undef MTG_DL_LDS
+  return lds > 0 && lds <= kMaxLdsHard;
 }
 
 hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream) {
@@ -22,6 +28,7 @@ hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream) {
 #define MTG_DL_CASE(NN, DD) \
   if (N == NN && a.D == DD) return launch_solve_dl_n##NN##_d##DD(a, stream);
   MTG_DL_CASE(10, 1) MTG_DL_CASE(10, 2) MTG_DL_CASE(10, 3) MTG_DL_CASE(10, 4)
+  MTG_DL_CASE(12, 1) MTG_DL_CASE(12, 2) MTG_DL_CASE(12, 3) MTG_DL_CASE(12, 4)
 #undef MTG_DL_CASE
   return hipErrorInvalidValue;
 }

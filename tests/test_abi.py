@@ -127,7 +127,9 @@ def test_solve_kernel_selection():
                            nat.MTG_KERNEL_SPLIT)
     L = nat.MTG_FLAG_DL_KERNEL
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_COLUMN_KERNEL) == col  # config 2 / 3, column A/B
-    assert lib.mtg_solve_kernel(12, 3, 20, 3, 0) == col  # config 4
+    assert lib.mtg_solve_kernel(12, 3, 20, 3, 0) == nat.MTG_KERNEL_DL  # config 4 (round 4)
+    assert lib.mtg_solve_kernel(12, 3, 20, 3, nat.MTG_FLAG_COLUMN_KERNEL) == col
+    assert lib.mtg_solve_kernel(12, 3, 18, 3, 0) == col  # the DL kernel is built for K = 20 at N = 12
     assert lib.mtg_solve_kernel(4, 3, 10, 1, 0) == col
     assert lib.mtg_solve_kernel(10, 3, 10, 4, L) == dl
     assert lib.mtg_solve_kernel(10, 1, 10, 1, L) == dl
@@ -138,7 +140,8 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(10, 3, 10, 0, L) == col   # r = 0: no translation trick
     for retired in (16, 32):
         assert lib.mtg_solve_kernel(10, 3, 10, 4, retired) == nat.MTG_KERNEL_DL
-    assert lib.mtg_solve_kernel(12, 3, 20, 3, L) == col
+    assert lib.mtg_solve_kernel(12, 3, 20, 3, L) == dl
+    assert lib.mtg_solve_kernel(12, 5, 20, 3, L) == col  # D > 4
     assert lib.mtg_solve_kernel(10, 3, 12, 4, 0) == gen   # G of 6 vertices exceeds both register budgets
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_SPLIT_KERNELS) == split
@@ -154,7 +157,7 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 10, nat.MTG_FLAG_DL_KERNEL) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 0, 125000, 0) == col  # r = 0: no translation trick
     assert lib.mtg_solve_kernel_batch(10, 3, 8, 4, 125000, 0) == col   # K != 10
-    assert lib.mtg_solve_kernel_batch(12, 3, 20, 3, 125000, 0) == col
+    assert lib.mtg_solve_kernel_batch(12, 3, 20, 3, 125000, 0) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 125000, nat.MTG_FLAG_SPLIT_KERNELS) == split
     assert nat.solve_kernel(10, 3, 10, 4, B=125000) == "solve_dl_kernel"
     assert lib.mtg_solve_kernel(10, 3, 50, 4, 0) == gen

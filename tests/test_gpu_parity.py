@@ -226,9 +226,10 @@ def test_paths_agree_mixed_masks(gpu_ctx):
 
 @pytest.mark.parametrize("K", [13, 17, 20])
 def test_wide_register_bucket_n12(gpu_ctx, K):
-    """N = 12, 12 < K <= 20 (config 4's shape) runs the register kernel's wide bucket (KMAX 20, G_v in
-    LDS, two waves per SIMD): against the general LDS-resident kernel and the oracle, with waypoint
-    masks (the IP fast path at K = 20) and with per-trajectory extra fixed derivatives (dense path)."""
+    """N = 12, 12 < K <= 20 (config 4's shape): the default path (K = 20: the dimension-lane kernel,
+    round 4) and the register kernel's wide bucket (KMAX 20, G_v in LDS, two waves per SIMD) against
+    the general LDS-resident kernel and the oracle, with waypoint masks (the fast paths at K = 20) and
+    with per-trajectory extra fixed derivatives (DL: those trajectories go through its fallback)."""
     O = _oracle()
     from mav_trajectory_generation_cmake_amd import random_vertices_batch
     B = 37  # ragged: 4 trajectories per wave
@@ -236,8 +237,8 @@ def test_wide_register_bucket_n12(gpu_ctx, K):
     rng = np.random.default_rng(K)
     mixed = mask.copy()
     mixed[:, 1:-1] |= (rng.integers(0, 2, size=mixed[:, 1:-1].shape) * 0x06).astype(np.uint8)
-    for m in (mask, mixed):
-        d = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True)
+    for m, kw in ((mask, {}), (mixed, {}), (mask, {"column": True}), (mixed, {"column": True})):
+        d = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True, **kw)
         g = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True, general=True)
         assert np.all(d["status"] == 0) and np.all(g["status"] == 0)
         assert scale_normalised_error(d["coeffs"], g["coeffs"], times) <= 1e-9
@@ -267,11 +268,11 @@ def test_wide_register_bucket_n12_dimensions(gpu_ctx, D, K):
     rng = np.random.default_rng(D * 100 + K)
     mixed = mask.copy()
     mixed[:, 1:-1] |= (rng.integers(0, 2, size=mixed[:, 1:-1].shape) * 0x06).astype(np.uint8)
-    for m in (mask, mixed):
-        d = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True)
+    for m, kw in ((mask, {}), (mixed, {}), (mask, {"column": True}), (mixed, {"column": True})):
+        d = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True, **kw)
         g = gpu_ctx.solve_linear_batch(12, 3, vals, m, times, status=True, cost=True, general=True)
         assert np.all(d["status"] == 0) and np.all(g["status"] == 0)
-        assert scale_normalised_error(d["coeffs"], g["coeffs"], times) <= 1e-9, (D, K)
+        assert scale_normalised_error(d["coeffs"], g["coeffs"], times) <= 1e-9, (D, K, kw)
         np.testing.assert_allclose(d["cost"], g["cost"], rtol=1e-9)
         ref = O.solve_linear_batch(12, 3, vals, m.astype(np.uint32), times)
         assert scale_normalised_error(d["coeffs"], ref, times) <= 1e-3
@@ -1151,3 +1152,42 @@ def test_result_independent_of_batch_composition(gpu_ctx, N, D, K, r):
         one = gpu_ctx.solve_linear_batch(N, r, vals[b:b + 1], mask[b:b + 1], times[b:b + 1], **kw)
         for k in keys:
             np.testing.assert_array_equal(one[k], whole[k][b:b + 1], err_msg="single %d %s" % (b, k))
+
+
+def test_config4_full_size_dl_vs_column(gpu_ctx):
+    """Config 4 at full size (1e4 x N = 12, K = 20, JERK, createRandomVertices(SNAP, 20, [-10,-20,-10],
+    [10,20,10]) + estimateSegmentTimes(3, 5)): the default path is the dimension-lane kernel with the
+    end vertices' free fifth derivative (round 4).  Against the column kernel's wide bucket: every
+    trajectory within 1e-8 scale-normalised, or arbitrated by 60-digit truth (the DL kernel within 1e-9
+    of truth or closer to it than the column kernel); checkPath (relative) on all; free values (including
+    the end vertices' free derivative), n_free, cost and status."""
+    import os
+    import sys
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch
+    N, K, r, B = 12, 20, 3, 10000
+    assert nat.solve_kernel(N, 3, K, r, B=B) == "solve_dl_kernel"
+    vals, mask, times = random_vertices_batch(N, 3, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=0,
+                                              max_derivative=4, v_max=3.0, a_max=5.0)
+    kw = dict(free=True, n_free=True, cost=True, status=True)
+    dl = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    col = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, column=True, **kw)
+    assert np.all(dl["status"] == 0) and np.all(col["status"] == 0)
+    np.testing.assert_array_equal(dl["n_free"], col["n_free"])
+    assert int(dl["n_free"][0]) == 2 + (K - 1) * 5
+    assert check_path(vals, mask, times, dl["coeffs"], N, relative=True) < 1e-6
+    errs = np.array([scale_normalised_error(dl["coeffs"][b:b + 1], col["coeffs"][b:b + 1], times[b:b + 1])
+                     for b in range(B)])
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_golden import truth_solve
+    arb = sorted(set(np.nonzero(errs > 1e-8)[0].tolist()) | {int(np.argmax(errs))})
+    assert len(arb) <= 20, (len(arb), np.sort(errs)[-5:])
+    for b in arb[:20]:
+        tr = truth_solve(N, r, vals[b], mask[b], times[b])[0][None]
+        e_dl = scale_normalised_error(dl["coeffs"][b:b + 1], tr, times[b:b + 1])
+        e_col = scale_normalised_error(col["coeffs"][b:b + 1], tr, times[b:b + 1])
+        assert e_dl <= max(1e-9, e_col), (b, e_dl, e_col)
+    np.testing.assert_allclose(dl["cost"], col["cost"], rtol=1e-8)
+    nf = int(dl["n_free"][0])
+    fs = np.max(np.abs(col["free"][:, :, :nf]), axis=2, keepdims=True)
+    assert np.max(np.abs(dl["free"][:, :, :nf] - col["free"][:, :, :nf]) / fs) <= 1e-7
