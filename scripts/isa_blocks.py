@@ -29,7 +29,7 @@ def main():
     blocks = []
     cur = None
     for l in body:
-        m = re.match(r"^(\.LBB\S+):", l)
+        m = re.match(r"^(\.LBB\S+):", l) or re.match(r"^; (%bb\.\d+):", l)
         if m or cur is None:
             cur = {"name": m.group(1) if m else "entry", "all": 0, "v": 0, "f64": 0, "s": 0, "ds": 0, "glb": 0,
                    "br": []}
