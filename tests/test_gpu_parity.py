@@ -440,7 +440,9 @@ def test_vertex_maps_vs_oracle(gpu_ctx):
         sol = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, free=True)
         xf = full_vertex_values(vals, mask, sol["free"], N)
         c = gpu_ctx.coefficients_from_vertices_batch(N, xf, times)
-        assert scale_normalised_error(c, sol["coeffs"], times) <= 1e-12, N
+        # (the DL kernel forms its coefficients in its scaled basis and hands out the unscaled free
+        # values: the two routes differ by rounding, 2.4e-12 on these batches)
+        assert scale_normalised_error(c, sol["coeffs"], times) <= 1e-11, N
         x2 = gpu_ctx.vertex_derivatives_batch(sol["coeffs"], times)
         scale = np.max(np.abs(xf), axis=(1, 2), keepdims=True)  # per trajectory and dimension
         assert np.max(np.abs(x2 - xf) / scale) <= 1e-9, N
@@ -974,7 +976,8 @@ def test_dl_kernel_vs_column_and_oracle(gpu_ctx, D, r):
     """The dimension-lane kernel (MTG_FLAG_DL_KERNEL): the reference generators' pattern against the
     column kernel (1e-8, scale-normalised: the host path and the oracle differ by up to 1.4e-8 on these
     batches) and the oracle; free values, n_free, cost and status; a ragged last wave; a wave whose
-    masks break the pattern runs the general kernel's block function inside it, bit-identical to it."""
+    trajectory whose masks break the pattern is solved by the general kernel's block function inside
+    it, bit-identical to the general kernel, and its wave-mates are unaffected."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
     O = _oracle()
@@ -999,19 +1002,21 @@ def test_dl_kernel_vs_column_and_oracle(gpu_ctx, D, r):
     ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
     assert scale_normalised_error(dl["coeffs"], ref, times) <= 1e-6
     assert check_path(vals, mask, times, dl["coeffs"], N, relative=True) < 1e-6
-    # a wave with another pattern: trajectory 2 tpw + 1 fixes a velocity at vertex 2
+    # another pattern: trajectory 2 tpw + 1 fixes a velocity at vertex 2.  It alone is solved by the
+    # general kernel's block function (the fallback), with that kernel's bits; every other trajectory,
+    # its wave-mates included, keeps the bits it had without it (round 4: per trajectory, not per wave)
     m2 = mask.copy()
-    m2[2 * tpw + 1, 2] |= 2
+    bad = 2 * tpw + 1
+    m2[bad, 2] |= 2
     dl2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, dl=True, **kw)
     col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, general=True, **kw)
-    w = slice(2 * tpw, 3 * tpw)
-    for k in ("coeffs", "cost", "free", "status"):
+    others = np.arange(B) != bad
+    for k in ("coeffs", "cost", "free", "status", "n_free"):
         if k == "cost":  # (the general kernel sums the cost over its 8 or 16 lanes: 1-ulp differences)
-            np.testing.assert_allclose(dl2[k][w], col2[k][w], rtol=1e-14, err_msg=k)
+            np.testing.assert_allclose(dl2[k][bad], col2[k][bad], rtol=1e-14, err_msg=k)
         else:
-            np.testing.assert_array_equal(dl2[k][w], col2[k][w], err_msg=k)
-        np.testing.assert_array_equal(dl2[k][:2 * tpw], dl[k][:2 * tpw], err_msg=k)
-        np.testing.assert_array_equal(dl2[k][3 * tpw:], dl[k][3 * tpw:], err_msg=k)
+            np.testing.assert_array_equal(dl2[k][bad], col2[k][bad], err_msg=k)
+        np.testing.assert_array_equal(dl2[k][others], dl[k][others], err_msg=k)
 
 
 def test_dl_kernel_time_sweep_status_and_device_outputs(gpu_ctx):
