@@ -61,4 +61,12 @@ res = {"B": B, "N": N, "K": K, "waves": int(len(w)), "span_us": float(rel[:, 4].
        "simds_used": len(per_simd),
        "simds_by_wave_count": {int(k): int(v) for k, v in sorted(collections.Counter(per_simd.values()).items())},
        "waves_per_xcd": {int(k): int(v) for k, v in sorted(collections.Counter(xcc).items())}}
+# per XCD, relative to its own first wave (the XCDs' clocks may be offset)
+res["per_xcd"] = {}
+for x in sorted(set(xcc.tolist())):
+    sel = xcc == x
+    s0 = st[sel, 0].min()
+    res["per_xcd"][int(x)] = {"start_p50_us": float(np.percentile(st[sel, 0] - s0, 50) / 100),
+                              "start_max_us": float((st[sel, 0] - s0).max() / 100),
+                              "span_us": float((st[sel, 4] - s0).max() / 100)}
 print(json.dumps(res))
