@@ -28,6 +28,21 @@ constexpr size_t kMaxLdsHard = 160 * 1024;
 // HBM write latency once per round.
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// A buffer resource over [base, base + bytes), built from wave-uniform values (readfirstlane, so the
+// compiler keeps it in SGPRs and emits no waterfall loop around the buffer instructions).  Loads and
+// stores address it with 32-bit per-lane byte offsets; a store whose offset is past `bytes` is
+// dropped by the hardware, which is how a lane skips a store without a branch.
+constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past any resource this code builds
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+  void* q = reinterpret_cast<void*>(((uintptr_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 // Native 2 x f64 vector (HIP's double2 is a struct: arrays of it in registers can fall back to
 // private memory where a vector type stays in VGPRs).
 typedef double dvec2 __attribute__((ext_vector_type(2)));

@@ -60,20 +60,37 @@ struct Prog {
 
 constexpr int64_t kTwo53 = 9007199254740992LL;
 
-// floor(num / den) for 0 <= num < 2^62, 0 < den < 2^62: v_rcp_f64 refined by one Newton step
-// (multiply and subtract, not fused), then corrected to the exact integer quotient.  ~4x cheaper
-// than the int64 division emulation, and the run arithmetic is the serial part of the clock.
-__device__ __forceinline__ int64_t floor_div(int64_t num, int64_t den) {
+// 1/den to a few ulp (v_rcp_f64 and one Newton step, multiply and subtract: not fused, so the
+// kernel's only f64 FMAs stay the compiler's conversion idiom, tests/test_build.py), for
+// floor_div_r: the two limits of a progression share its increment, so they share the reciprocal.
+__device__ __forceinline__ double recip(int64_t den) {
 #pragma clang fp contract(off)
   const double dd = (double)den;
-  double y = __builtin_amdgcn_rcp(dd);
-  y = y * (2.0 - dd * y);
+  const double y = __builtin_amdgcn_rcp(dd);
+  return y * (2.0 - dd * y);
+}
+
+// floor(num / den) for 0 <= num < 2^62, 0 < den < 2^62, given y = recip(den).  The estimate's error
+// is ~q 2^-48 + 1, so one correction each way is exact for q < 2^45 (a run of 2^45 samples); the
+// loops are the guard beyond that.  (Round 3 corrected by loops alone, each iteration a 64-bit
+// multiply and an exec-mask round trip for the wave.)
+__device__ __forceinline__ int64_t floor_div_r(int64_t num, int64_t den, double y) {
   double qd = (double)num * y;
-  if (qd > 4.0e18) qd = 4.0e18;
+  qd = qd < 4.0e18 ? qd : 4.0e18;
   int64_t q = (int64_t)qd;
-  if (q < 0) q = 0;
-  while (q > 0 && q * den > num) --q;
-  while ((q + 1) * den <= num) ++q;
+  q = q < 0 ? 0 : q;
+  int64_t r = num - q * den;
+  if (r < 0) {
+    --q;
+    r += den;
+  } else if (r >= den) {
+    ++q;
+    r -= den;
+  }
+  if (__builtin_expect(r < 0 || r >= den, 0)) {
+    while (q > 0 && q * den > num) --q;
+    while ((q + 1) * den <= num) ++q;
+  }
   return q;
 }
 
@@ -117,14 +134,6 @@ __device__ __forceinline__ double prog_value(const Prog& p, int64_t k) { return 
 
 constexpr int64_t kNoLimit = (int64_t)1 << 62;
 
-// number of k >= 0 with m + k inc <= lim (lim given as a double, exact if < 2^62, else no limit)
-__device__ __forceinline__ int64_t run_len_le(const Prog& p, double lim_scaled) {
-  if (!(lim_scaled < 4.0e18)) return kNoLimit;
-  const int64_t lim = (int64_t)lim_scaled;
-  if (lim < p.m) return 0;
-  return floor_div(lim - p.m, p.inc) + 1;
-}
-
 // One run of the clock: samples n0 .. n0+L-1 at tin = prog_value(t, k), acc = prog_value(a, k)
 // (L == 1 and single: the plain doubles tin0 / acc0), all in segment seg.
 struct Run {
@@ -135,7 +144,25 @@ struct Run {
   bool single;
 };
 
+// number of k >= 0 with m + k inc <= lim (lim given as a double, exact if < 2^62, else no limit),
+// given y = recip(p.inc)
+__device__ __forceinline__ int64_t run_len_le_r(const Prog& p, double lim_scaled, double y) {
+  if (!(lim_scaled < 4.0e18)) return kNoLimit;
+  const int64_t lim = (int64_t)lim_scaled;
+  if (lim < p.m) return 0;
+  return floor_div_r(lim - p.m, p.inc, y) + 1;
+}
+
 // The reference's clock (src/trajectory.cpp:86-127), advanced run by run.
+//
+// A run ends where the first of four limits is reached: tin leaves its binade, tin > T_i, acc leaves
+// its binade, acc >= t_end.  The clock is one lane's serial chain, and the lanes of a wave run the
+// union of their paths, so every call of next() does the same work on every lane: one run, then the
+// reference's end-of-step checks -- acc >= t_end, and the segment switches (tin > T_i: tin -= T_i)
+// -- folded into the same call rather than taken as a loop iteration of their own, which cost the
+// whole wave a second run iteration whenever any of its lanes switched (round 3).  (Carrying the
+// progressions from run to run instead of re-deriving them saves no time for the same reason: some
+// lane of the wave re-derives each of them at almost every run.)
 struct Clock {
   const double* T;
   int K;
@@ -145,6 +172,22 @@ struct Clock {
   int64_t n;
   bool done;
 
+  // the reference's checks before a sample: stop at t_end, switch segments while tin > T_i
+  __device__ __forceinline__ void settle() {
+    if (!(acc < t_end)) {
+      done = true;
+      return;
+    }
+    while (tin > Ti) {  // segment switch: no sample, acc unchanged
+      tin = tin - Ti;
+      if (++seg >= K) {
+        done = true;
+        return;
+      }
+      Ti = T[seg];
+    }
+  }
+
   __device__ __forceinline__ void init(const double* tms, int K_, double t_start, double t_end_, double dt_) {
     T = tms;
     K = K_;
@@ -153,53 +196,41 @@ struct Clock {
     n = 0;
     done = !range_start(tms, K, t_start, &seg, &acc, &tin);
     Ti = done ? 0.0 : T[seg];
+    if (!done) settle();
   }
 
   // next run into *r; false when the clock has stopped
   __device__ __forceinline__ bool next(Run* r) {
-    while (!done) {
-      if (!(acc < t_end)) {
-        done = true;
-        break;
+    if (done) return false;
+    r->n0 = n;
+    r->seg = seg;
+    r->tin0 = tin;
+    r->acc0 = acc;
+    Prog pt, pa;
+    int64_t L = 1;
+    r->single = true;
+    if (progression(tin, dt, &pt) && progression(acc, dt, &pa)) {
+      const double yt = recip(pt.inc), ya = recip(pa.inc);
+      int64_t lim = floor_div_r(kTwo53 - 1 - pt.m, pt.inc, yt) + 1;                         // tin binade
+      lim = min(lim, floor_div_r(kTwo53 - 1 - pa.m, pa.inc, ya) + 1);                         // acc binade
+      lim = min(lim, run_len_le_r(pt, __builtin_amdgcn_ldexp(Ti, -pt.E), yt));               // tin <= T_i
+      const double q = __builtin_amdgcn_ldexp(t_end, -pa.E);                                 // acc < t_end
+      if (q < 4.0e18) lim = min(lim, run_len_le_r(pa, __builtin_ceil(q) - 1.0, ya));
+      L = lim < 1 ? 1 : lim;
+      r->t = pt;
+      r->a = pa;
+      r->single = false;
+      if (L > 1) {  // state at the run's last sample, exactly
+        tin = prog_value(pt, L - 1);
+        acc = prog_value(pa, L - 1);
       }
-      if (tin > Ti) {  // segment switch: no sample, acc unchanged
-        tin = tin - Ti;
-        if (++seg >= K) {
-          done = true;
-          break;
-        }
-        Ti = T[seg];
-        continue;
-      }
-      r->n0 = n;
-      r->seg = seg;
-      r->tin0 = tin;
-      r->acc0 = acc;
-      Prog pt, pa;
-      int64_t L = 1;
-      r->single = true;
-      if (progression(tin, dt, &pt) && progression(acc, dt, &pa)) {
-        int64_t lim = floor_div(kTwo53 - 1 - pt.m, pt.inc) + 1;                             // tin binade
-        lim = min(lim, floor_div(kTwo53 - 1 - pa.m, pa.inc) + 1);                              // acc binade
-        lim = min(lim, run_len_le(pt, __builtin_amdgcn_ldexp(Ti, -pt.E)));                     // tin <= T_i
-        const double q = __builtin_amdgcn_ldexp(t_end, -pa.E);                                 // acc < t_end
-        if (q < 4.0e18) lim = min(lim, run_len_le(pa, __builtin_ceil(q) - 1.0));
-        L = lim < 1 ? 1 : lim;
-        r->t = pt;
-        r->a = pa;
-        r->single = false;
-        if (L > 1) {  // state at the run's last sample, exactly
-          tin = prog_value(pt, L - 1);
-          acc = prog_value(pa, L - 1);
-        }
-      }
-      r->L = L;
-      n += L;
-      tin += dt;  // the step after the run's last sample, as the reference takes it
-      acc += dt;
-      return true;
     }
-    return false;
+    r->L = L;
+    n += L;
+    tin += dt;  // the step after the run's last sample, as the reference takes it
+    acc += dt;
+    settle();
+    return true;
   }
 };
 
@@ -328,8 +359,11 @@ __global__ __launch_bounds__(kScanThreads) void eval_scan_kernel(int64_t nb, int
 constexpr int kRuns = 64;
 constexpr int kEvalThreads = 64;
 
+// (A run's length is the next run's n0 less its own.  Config 2, K = 10, D = 3, N = 10: this table
+// 4.6 KB + the Horner terms 2.4 KB + the staged block 3 KB = 10 KB per wave, so 16 waves -- 4 per
+// SIMD, amdgpu_waves_per_eu below -- fit in a CU's 160 KB.)
 struct RunLds {  // structure of arrays in LDS
-  int64_t n0[kRuns], L[kRuns], tm[kRuns], ti[kRuns], am[kRuns], ai[kRuns];
+  int64_t n0[kRuns], tm[kRuns], ti[kRuns], am[kRuns], ai[kRuns];
   double tin0[kRuns], acc0[kRuns];
   int tE[kRuns], aE[kRuns], seg[kRuns], single[kRuns];
 };
@@ -340,8 +374,14 @@ struct RunLds {  // structure of arrays in LDS
 // DER >= 0: the derivative order at compile time (0..4, the common ones); DER < 0: `derivative`.
 // DD > 0: D at compile time (the sample loop takes kSpl samples per lane per block); 0: D at run time.
 constexpr int kSpl = 2;
+#ifndef MTG_EVAL_EXP
+#define MTG_EVAL_EXP 0  // (diagnostic builds only: 1 no run lookup, 2 no Horner, 3 stores dropped)
+#endif
+#ifndef MTG_EVAL_WAVES
+#define MTG_EVAL_WAVES 4
+#endif
 template <int N, int DER, int DD>
-__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3))) void eval_range_kernel(int D, int K, const double* coeffs,
+__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MTG_EVAL_WAVES))) void eval_range_kernel(int D, int K, const double* coeffs,
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
@@ -365,6 +405,14 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
   RunLds* rt = reinterpret_cast<RunLds*>(lds);
   double* cf = reinterpret_cast<double*>(rt + 1);  // [K][D][N]
   double* ob = cf + K * D * N;                     // [kEvalThreads][D] output block
+  // The D-at-compile-time sample loop stores through buffer resources over this trajectory's rows and
+  // sample times, addressed by 32-bit byte offsets (a trajectory with under 2 GiB of rows; longer
+  // ones take the run-time-D loop), with 16-B pieces when `out` is 16-B aligned.
+  const bool fast = DD > 0 && n_total * (int64_t)(D * 8) < (int64_t)kBufOOB;
+  const bool al16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out + base * D, fast ? (uint32_t)(n_total * D * 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rs =
+      buf_rsrc(sample_times ? sample_times + base : out, fast && sample_times ? (uint32_t)(n_total * 8) : 0u);
   const double* cb = coeffs + b * (int64_t)K * D * N;
   if (DER >= 0) derivative = DER;
   // the Horner terms base_coefficients_(derivative, j) * coefficients_[j] (polynomial.h:143-148) do
@@ -400,7 +448,6 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
       if (lane < nr) {
         const RunRec w = rr[next_run + lane];
         rt->n0[lane] = w.n0;
-        rt->L[lane] = w.L;
         rt->tm[lane] = w.tm;
         rt->ti[lane] = w.ti;
         rt->tE[lane] = w.tE;
@@ -420,7 +467,6 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
       Run r;
       while (nr < kRuns && ck.next(&r)) {
         rt->n0[nr] = r.n0;
-        rt->L[nr] = r.L;
         rt->tm[nr] = r.t.m;
         rt->ti[nr] = r.t.inc;
         rt->tE[nr] = r.t.E;
@@ -436,32 +482,40 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
       s_nr = nr;
       s_end = ck.n;
     }
-    __syncthreads();
+    lds_fence();  // (one wave per block: the table is complete for every lane)
     const int nr = s_nr;
     if (nr == 0) break;
     const int64_t first = rt->n0[0], end = s_end < n_total ? s_end : n_total;
     int ri = 0;
-    if constexpr (DD > 0) {
+    if (DD > 0 && fast) {
       // D at compile time: each lane takes kSpl samples per block (n = nb + s 64 + lane), and their
       // kSpl D Horner chains are independent, so they interleave instead of running one dimension
       // after the other; the staged rows are read back in one batch before the stores.
       constexpr int kBlk = kSpl * kEvalThreads;
+      constexpr int DDc = DD > 0 ? DD : 1;
+      // 16-B row pieces: a full block's kBlk DD doubles are kBlk DD / 128 pieces per lane
+      constexpr int P16 = kBlk * DDc / (2 * kEvalThreads);
       int64_t nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;  // the next run's first sample
-      double cc[DD * N];  // the cached segment's Horner terms (wave-uniform)
+      double cc[DDc * N];  // the cached segment's Horner terms (wave-uniform: SGPRs)
       int cseg = -1;
-      for (int64_t nb = first; nb < end; nb += kBlk) {
-        const int cnt = (int)(end - nb < kBlk ? end - nb : kBlk);
+      for (int64_t nb = first; nb < end;) {
+        // blocks start where the rows are 16-B aligned in `out` (an odd D: (base + nb) even), so a
+        // full block leaves in 16-B pieces; the round's first block may be one sample short
+        int cnt = (int)(end - nb < kBlk ? end - nb : kBlk);
+        if ((DDc & 1) && (((base + nb) & 1) != 0) && cnt == kBlk) cnt = kBlk - 1;
         double tv[kSpl];
         const double* cs[kSpl];
         int sg[kSpl];
 #pragma unroll
         for (int s = 0; s < kSpl; ++s) {
           const int64_t n = nb + s * kEvalThreads + lane;
-          const bool have = n < end;
+          const bool have = s * kEvalThreads + lane < cnt;
+#if MTG_EVAL_EXP != 1
           while (have && nxt <= n) {
             ++ri;
             nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;
           }
+#endif
           const int64_t k = n - rt->n0[ri];
           double t, a;
           if (rt->single[ri]) {
@@ -471,31 +525,49 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
             t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
             a = sample_times ? mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]) : 0.0;
           }
+#if MTG_EVAL_EXP == 1
+          t = (double)n * 1e-3;
+          a = t;
+#endif
           tv[s] = t;
           sg[s] = rt->seg[ri];
-          cs[s] = cf + (sg[s] * DD) * N;
-          if (sample_times && have) sample_times[base + n] = a;
+          cs[s] = cf + (sg[s] * DDc) * N;
+          if (sample_times)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), rs, have && MTG_EVAL_EXP != 3 ? (uint32_t)(n * 8) : kBufOOB, 0, 0);
         }
-        double v[kSpl][DD];
+        double v[kSpl][DDc];
         // Usually the whole block lies in one segment (a segment has ~750 samples at dt = 0.01): its
-        // coefficients then come from registers, reloaded from LDS only when the wave's segment
-        // changes.  Per-lane LDS reads of every coefficient for every sample made the CU's LDS
-        // bandwidth the limit (~30 16-B reads per lane per block).
+        // Horner terms then come from SGPRs (read from LDS only when the wave's segment changes),
+        // which leaves the VGPRs to the samples.  Per-lane LDS reads of every coefficient for every
+        // sample made the CU's LDS bandwidth the limit (~30 16-B reads per lane per block).
         const int sg0 = __builtin_amdgcn_readfirstlane(sg[0]);
         bool same = true;
 #pragma unroll
         for (int s = 0; s < kSpl; ++s) same = same && sg[s] == sg0;
+#if MTG_EVAL_EXP == 2
+        if (true) {
+#pragma unroll
+          for (int s = 0; s < kSpl; ++s)
+#pragma unroll
+            for (int d = 0; d < DDc; ++d) v[s][d] = tv[s] + d;
+        } else
+#endif
         if (__builtin_amdgcn_ballot_w64(!same) == 0) {
           if (sg0 != cseg) {
-            const double* c0 = cf + (sg0 * DD) * N;
+            const double* c0 = cf + (sg0 * DDc) * N;
 #pragma unroll
-            for (int i = 0; i < DD * N; ++i) cc[i] = c0[i];
+            for (int i = 0; i < DDc * N; ++i) {
+              const uint64_t w = __builtin_bit_cast(uint64_t, c0[i]);
+              const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+              const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)w);
+              cc[i] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+            }
             cseg = sg0;
           }
 #pragma unroll
           for (int s = 0; s < kSpl; ++s)
 #pragma unroll
-            for (int d = 0; d < DD; ++d) v[s][d] = derivative < N ? cc[d * N + N - 1] : 0.0;
+            for (int d = 0; d < DDc; ++d) v[s][d] = derivative < N ? cc[d * N + N - 1] : 0.0;
           if (derivative < N) {
 #pragma unroll
             for (int j = N - 2; j >= 0; --j) {
@@ -503,7 +575,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
 #pragma unroll
                 for (int s = 0; s < kSpl; ++s)
 #pragma unroll
-                  for (int d = 0; d < DD; ++d) {
+                  for (int d = 0; d < DDc; ++d) {
                     v[s][d] = v[s][d] * tv[s];
                     v[s][d] = v[s][d] + cc[d * N + j];
                   }
@@ -514,7 +586,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
 #pragma unroll
           for (int s = 0; s < kSpl; ++s)
 #pragma unroll
-            for (int d = 0; d < DD; ++d) v[s][d] = derivative < N ? cs[s][d * N + N - 1] : 0.0;
+            for (int d = 0; d < DDc; ++d) v[s][d] = derivative < N ? cs[s][d * N + N - 1] : 0.0;
           if (derivative < N) {
 #pragma unroll
             for (int j = N - 2; j >= 0; --j) {
@@ -522,7 +594,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
 #pragma unroll
                 for (int s = 0; s < kSpl; ++s)
 #pragma unroll
-                  for (int d = 0; d < DD; ++d) {
+                  for (int d = 0; d < DDc; ++d) {
                     v[s][d] = v[s][d] * tv[s];
                     v[s][d] = v[s][d] + cs[s][d * N + j];
                   }
@@ -533,19 +605,35 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
 #pragma unroll
         for (int s = 0; s < kSpl; ++s)
 #pragma unroll
-          for (int d = 0; d < DD; ++d) ob[(s * kEvalThreads + lane) * DD + d] = v[s][d];
+          for (int d = 0; d < DDc; ++d) ob[(s * kEvalThreads + lane) * DDc + d] = v[s][d];
         lds_fence();  // one wave per block: the staged rows are complete
-        double* dst = out + (base + nb) * DD;
-        double w[kSpl * DD];
+#if MTG_EVAL_EXP == 3
+        const uint32_t o0 = kBufOOB;
+#else
+        const uint32_t o0 = (uint32_t)(nb * DDc * 8);  // the block's first row, bytes into the trajectory's rows
+#endif
+        if (cnt == kBlk && al16) {  // whole 16-B pieces, 1 KiB per store instruction
+          dvec2 w[P16];
 #pragma unroll
-        for (int u = 0; u < kSpl * DD; ++u) w[u] = ob[u * kEvalThreads + lane];
-        lds_fence();  // (read before the next block overwrites them)
+          for (int u = 0; u < P16; ++u) w[u] = *reinterpret_cast<const dvec2*>(ob + 2 * (u * kEvalThreads + lane));
+          lds_fence();  // (read before the next block overwrites them)
 #pragma unroll
-        for (int u = 0; u < kSpl * DD; ++u)
-          if (u * kEvalThreads + lane < cnt * DD) dst[u * kEvalThreads + lane] = w[u];
+          for (int u = 0; u < P16; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w[u]), ro, o0 + (uint32_t)(u * kEvalThreads + lane) * 16, 0, 0);
+        } else {
+          double w[kSpl * DDc];
+#pragma unroll
+          for (int u = 0; u < kSpl * DDc; ++u) w[u] = ob[u * kEvalThreads + lane];
+          lds_fence();
+#pragma unroll
+          for (int u = 0; u < kSpl * DDc; ++u)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, w[u]), ro,
+                                                  u * kEvalThreads + lane < cnt * DDc ? o0 + (uint32_t)(u * kEvalThreads + lane) * 8 : kBufOOB, 0, 0);
+        }
+        nb += cnt;
       }
       if (end >= n_total) break;
-      __syncthreads();  // the run table is refilled next
+      lds_fence();  // the run table is refilled next (one wave: no barrier, no wait on the stores)
       continue;
     }
     for (int64_t nb = first; nb < end; nb += kEvalThreads) {
@@ -580,11 +668,11 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(3)
         }
         if (sample_times) sample_times[base + n] = a;
       }
-      __syncthreads();
+      lds_fence();
       // the block's rows are contiguous in out: write them with consecutive lanes
       double* dst = out + (base + nb) * D;
       for (int i = lane; i < cnt * D; i += kEvalThreads) dst[i] = ob[i];
-      __syncthreads();
+      lds_fence();
     }
     if (end >= n_total) break;
   }

@@ -81,19 +81,21 @@ t_count, _ = timed(count)
 t_run, kms = timed(run)
 t_full, kms_full = timed(full)
 # the one-call outputs equal the two-call ones; spot-check against the oracle's evaluateRange (bit-exact)
-assert int(ft_d.item()) == total
-assert torch.equal(fc_d, cnt_d) and torch.equal(fo_d, o_d)
-assert torch.equal(fout_d[:total], out_d) and torch.equal(fst_d[:total], st_d)
-from oracle import pyoracle as O  # noqa: E402
-out = out_d.cpu().numpy()
-st = st_d.cpu().numpy()
-for b in (0, B // 2, B - 1):
-    ro, rst, n = O.evaluate_range(coeffs[b], times[b], 0.0, t_end, dt, 0, max_samples=int(counts[b]) + 10)
-    assert n == counts[b] and np.array_equal(out[offs[b]:offs[b] + n], ro) and np.array_equal(st[offs[b]:offs[b] + n], rst)
+# (NOCHECK=1: timing only, for diagnostic builds that compute something else)
+if not os.environ.get("NOCHECK"):
+    assert int(ft_d.item()) == total
+    assert torch.equal(fc_d, cnt_d) and torch.equal(fo_d, o_d)
+    assert torch.equal(fout_d[:total], out_d) and torch.equal(fst_d[:total], st_d)
+    from oracle import pyoracle as O  # noqa: E402
+    out = out_d.cpu().numpy()
+    st = st_d.cpu().numpy()
+    for b in (0, B // 2, B - 1):
+        ro, rst, n = O.evaluate_range(coeffs[b], times[b], 0.0, t_end, dt, 0, max_samples=int(counts[b]) + 10)
+        assert n == counts[b] and np.array_equal(out[offs[b]:offs[b] + n], ro) and np.array_equal(st[offs[b]:offs[b] + n], rst)
 bytes_out = total * (D + 1) * 8
 print(json.dumps({"B": B, "samples": total, "samples_per_traj": total / B,
                   "full_call_ms_wall": t_full * 1e3, "full_call_gpu_ms": kms_full,
-                  "full_samples_per_s": total / (t_full * 1e-3 if t_full > kms_full * 1e-3 else kms_full * 1e-3),
+                  "full_samples_per_s": total / max(t_full, kms_full * 1e-3),
                   "full_out_GBps": bytes_out / (kms_full * 1e-3) / 1e9, "full_frac_hbm": bytes_out / (kms_full * 1e-3) / 8e12,
                   "two_call": {"count_ms_wall": t_count * 1e3, "eval_ms_wall": t_run * 1e3, "eval_gpu_ms": kms},
                   "note": "full_call_gpu_ms: HIP events around the call's kernels (clock+count, scan, samples); "
