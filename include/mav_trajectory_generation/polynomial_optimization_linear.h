@@ -458,17 +458,21 @@ class PolynomialOptimization {
     mask_.assign(V, 0);
     std::vector<int> fixed_rank((size_t)V * h, -1), free_rank((size_t)V * h, -1);
     int nf = 0, np = 0;
-    for (int v = 0; v < V; ++v)
+    for (int v = 0; v < V; ++v) {
+      // the vertex's constraints in derivative order (a std::map), read in place
+      auto it = vertices_[v].cBegin();
+      const auto end = vertices_[v].cEnd();
       for (int k = 0; k < h; ++k) {
-        VectorXd value;
-        if (vertices_[v].getConstraint(k, &value)) {
+        while (it != end && it->first < k) ++it;
+        if (it != end && it->first == k) {
           mask_[v] |= (uint8_t)(1u << k);
-          for (int d = 0; d < D; ++d) values_[((size_t)v * h + k) * D + d] = value[d];
+          for (int d = 0; d < D; ++d) values_[((size_t)v * h + k) * D + d] = it->second[d];
           fixed_rank[(size_t)v * h + k] = nf++;
         } else {
           free_rank[(size_t)v * h + k] = np++;
         }
       }
+    }
     n_fixed_constraints_ = nf;
     n_free_constraints_ = np;
     n_all_constraints_ = (size_t)N * n_segments_;  // ends once, interior vertices twice
@@ -511,15 +515,17 @@ class PolynomialOptimization {
     setSegmentsFromCoefficients(coeffs);
   }
 
+  // (the segments' polynomials, order N since setupFromVertices, take the coefficients into their own
+  // storage: one buffer per call instead of a vector and a polynomial per segment and dimension)
   void setSegmentsFromCoefficients(const std::vector<double>& coeffs) {
     const int D = (int)dimension_;
+    VectorXd c(N);
     for (size_t i = 0; i < n_segments_; ++i) {
       Segment& s = segments_[i];
       s.setTime(segment_times_[i]);
       for (int d = 0; d < D; ++d) {
-        VectorXd c(N);
         for (int j = 0; j < N; ++j) c[j] = coeffs[(i * D + d) * N + j];
-        s[d] = Polynomial(N, c);
+        s[d].setCoefficients(c);
       }
     }
   }

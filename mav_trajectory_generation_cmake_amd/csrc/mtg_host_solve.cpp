@@ -60,11 +60,12 @@ struct HostSolve {
   static constexpr int H = N / 2;
   static constexpr unsigned HM = (1u << H) - 1u;
 
-  // LDL^T of the h x h pinned S (lower triangle used), in place; returns the smallest pivot.
-  static double ldlt(double (&S)[H][H], double (&dinv)[H]) {
+  // LDL^T of the leading n x n block of S (the free derivatives of a vertex; lower triangle used), in
+  // place; returns the smallest pivot.  ldlt_solve_n solves with it.
+  static double ldlt_n(double (&S)[H][H], double (&dinv)[H], int n) {
     double pmin = DBL_MAX;
     double dg[H];
-    for (int j = 0; j < H; ++j) {
+    for (int j = 0; j < n; ++j) {
       double w[H];
       double dj = S[j][j];
       for (int k = 0; k < j; ++k) {
@@ -75,7 +76,7 @@ struct HostSolve {
       const double inv = 1.0 / dj;
       dg[j] = dj;
       dinv[j] = inv;
-      for (int i = j + 1; i < H; ++i) {
+      for (int i = j + 1; i < n; ++i) {
         double t = S[i][j];
         for (int k = 0; k < j; ++k) t -= S[i][k] * w[k];
         S[i][j] = t * inv;
@@ -84,17 +85,31 @@ struct HostSolve {
     return pmin;
   }
 
-  static void ldlt_solve(const double (&S)[H][H], const double (&dinv)[H], double* x) {
+  static void ldlt_solve_n(const double (&S)[H][H], const double (&dinv)[H], double* x, int n) {
     double y[H];
-    for (int i = 0; i < H; ++i) {
+    for (int i = 0; i < n; ++i) {
       double t = x[i];
       for (int k = 0; k < i; ++k) t -= S[i][k] * y[k];
       y[i] = t;
     }
-    for (int i = H - 1; i >= 0; --i) {
+    for (int i = n - 1; i >= 0; --i) {
       double t = y[i] * dinv[i];
-      for (int k = i + 1; k < H; ++k) t -= S[k][i] * x[k];
+      for (int k = i + 1; k < n; ++k) t -= S[k][i] * x[k];
       x[i] = t;
+    }
+  }
+
+  // a vertex's D compressed vectors (its free entries first) to the full layout, pinned entries 0
+  static void expand(double* zv, int D, unsigned m) {
+    int fc[H], nc = 0;
+    for (int k = 0; k < H; ++k)
+      if (!((m >> k) & 1u)) fc[nc++] = k;
+    for (int d = 0; d < D; ++d) {
+      double* z = zv + (size_t)d * H;
+      double full[H];
+      for (int k = 0; k < H; ++k) full[k] = 0.0;
+      for (int a = 0; a < nc; ++a) full[fc[a]] = z[a];
+      for (int k = 0; k < H; ++k) z[k] = full[k];
     }
   }
 
@@ -214,92 +229,110 @@ struct HostSolve {
       }
     }
 
-    // forward sweep: S_v = D_v - E_{v-1}^T G_{v-1}, [G_v | z_v] = S_v^-1 [E_v | rhs_v]
+    // forward sweep: S_v = D_v - E_{v-1}^T G_{v-1}, [G_v | z_v] = S_v^-1 [E_v | rhs_v], over the free
+    // derivatives of each vertex only (fc[0..nc) at v, fp at v-1, fn at v+1): the pinned rows and
+    // columns of the symmetric pinning are identity rows with a zero right-hand side, so they add
+    // only exact zeros to the free entries' sums and their unknowns are 0 -- skipping them leaves
+    // every free entry's arithmetic, in the same order, unchanged.  G_v is [nc][nn] and z_v [D][nc]
+    // in the slots of the full layout; the solution is expanded to [V][D][H] afterwards.
     double pmin = DBL_MAX;
     int n_free = 0;
-    unsigned mp = 0, mc = m_of(0);
+    unsigned mc = m_of(0);
+    int fp[H], fc[H], fn[H], np_ = 0, nc = 0, nn = 0;
+    for (int k = 0; k < H; ++k)
+      if (!((mc >> k) & 1u)) fc[nc++] = k;
     for (int v = 0; v < V; ++v) {
-      const unsigned mn = v < K ? m_of(v + 1) : 0u;
-      n_free += __builtin_popcount(~mc & HM);
+      const unsigned mn = v < K ? m_of(v + 1) : HM;
+      nn = 0;
+      for (int k = 0; k < H; ++k)
+        if (!((mn >> k) & 1u)) fn[nn++] = k;
+      n_free += nc;
       double S[H][H];
-      for (int i = 0; i < H; ++i)
-        for (int j = 0; j < H; ++j) S[i][j] = 0.0;
-      // E_{v-1}^T (bottom-left block of H_{v-1}, rows at v-1 and columns at v pinned to zero)
-      double Et[H][H] = {};
+      double Et[H][H];  // E_{v-1}^T on the free rows at v and free columns at v-1
+      for (int i = 0; i < nc; ++i)
+        for (int j = 0; j <= i; ++j) S[i][j] = 0.0;
       if (v > 0) {
         const double* s = PW + (size_t)(v - 1) * H;
         const double f = SCl[v - 1];
-        for (int i = 0; i < H; ++i)
-          for (int j = 0; j <= i; ++j) S[i][j] += f * s[i] * s[j] * Ht[(H + i) * N + H + j];
-        for (int i = 0; i < H; ++i)    // row at v
-          for (int a = 0; a < H; ++a)  // column at v-1
-            Et[i][a] = (((mc >> i) | (mp >> a)) & 1u) ? 0.0 : f * s[i] * s[a] * Ht[(H + i) * N + a];
-        const double* Gp = G + (size_t)(v - 1) * H * H;  // Gp[a][j], a at v-1, j at v
-        for (int i = 0; i < H; ++i)
+        for (int i = 0; i < nc; ++i)
+          for (int j = 0; j <= i; ++j) S[i][j] += f * s[fc[i]] * s[fc[j]] * Ht[(H + fc[i]) * N + H + fc[j]];
+        for (int i = 0; i < nc; ++i)
+          for (int a = 0; a < np_; ++a) Et[i][a] = f * s[fc[i]] * s[fp[a]] * Ht[(H + fc[i]) * N + fp[a]];
+        const double* Gp = G + (size_t)(v - 1) * H * H;  // Gp[a][j], a free at v-1, j free at v
+        for (int i = 0; i < nc; ++i)
           for (int j = 0; j <= i; ++j) {
             double t = 0.0;
-            for (int a = 0; a < H; ++a) t += Et[i][a] * Gp[a * H + j];
+            for (int a = 0; a < np_; ++a) t += Et[i][a] * Gp[a * H + j];
             S[i][j] -= t;
           }
       }
       if (v < K) {
         const double* s = PW + (size_t)v * H;
         const double f = SCl[v];
-        for (int i = 0; i < H; ++i)
-          for (int j = 0; j <= i; ++j) S[i][j] += f * s[i] * s[j] * Ht[i * N + j];
-      }
-      for (int i = 0; i < H; ++i) {  // pin: identity rows and columns
-        if (!((mc >> i) & 1u)) continue;
-        for (int j = 0; j < H; ++j) S[i][j] = S[j][i] = 0.0;
-        S[i][i] = 1.0;
+        for (int i = 0; i < nc; ++i)
+          for (int j = 0; j <= i; ++j) S[i][j] += f * s[fc[i]] * s[fc[j]] * Ht[fc[i] * N + fc[j]];
       }
       double dinv[H];
-      const double pv = ldlt(S, dinv);
+      const double pv = nc ? ldlt_n(S, dinv, nc) : 1.0;
       pmin = (pv < pmin || pv != pv) ? pv : pmin;  // a NaN pivot sticks (NOT_SPD)
-      if (v < K) {  // G_v columns: E_v (top-right block of H_v) pinned
+      if (v < K) {  // G_v columns: E_v (top-right block of H_v) on the free rows and columns
         const double* s = PW + (size_t)v * H;
         const double f = SCl[v];
         double* Gv = G + (size_t)v * H * H;  // Gv[i][c]
-        for (int c = 0; c < H; ++c) {
+        for (int c = 0; c < nn; ++c) {
           double col[H];
-          for (int i = 0; i < H; ++i)
-            col[i] = (((mc >> i) | (mn >> c)) & 1u) ? 0.0 : f * s[i] * s[c] * Ht[i * N + H + c];
-          ldlt_solve(S, dinv, col);
-          for (int i = 0; i < H; ++i) Gv[i * H + c] = col[i];
+          for (int i = 0; i < nc; ++i) col[i] = f * s[fc[i]] * s[fn[c]] * Ht[fc[i] * N + H + fn[c]];
+          ldlt_solve_n(S, dinv, col, nc);
+          for (int i = 0; i < nc; ++i) Gv[i * H + c] = col[i];
         }
       }
       for (int d = 0; d < D; ++d) {
         double rhs[H];
-        for (int i = 0; i < H; ++i) {
+        for (int i = 0; i < nc; ++i) {
           double t = 0.0;
-          if (v > 0) t += Wp[((size_t)(v - 1) * D + d) * N + H + i];
-          if (v < K) t += Wp[((size_t)v * D + d) * N + i];
+          if (v > 0) t += Wp[((size_t)(v - 1) * D + d) * N + H + fc[i]];
+          if (v < K) t += Wp[((size_t)v * D + d) * N + fc[i]];
           if (v > 0) {
             const double* zp = Z + ((size_t)(v - 1) * D + d) * H;
-            for (int a = 0; a < H; ++a) t += Et[i][a] * zp[a];
+            for (int a = 0; a < np_; ++a) t += Et[i][a] * zp[a];
           }
-          rhs[i] = ((mc >> i) & 1u) ? 0.0 : -t;
+          rhs[i] = -t;
         }
-        ldlt_solve(S, dinv, rhs);
+        ldlt_solve_n(S, dinv, rhs, nc);
         double* z = Z + ((size_t)v * D + d) * H;
-        for (int i = 0; i < H; ++i) z[i] = rhs[i];
+        for (int i = 0; i < nc; ++i) z[i] = rhs[i];
       }
-      mp = mc;
       mc = mn;
+      np_ = nc;
+      nc = nn;
+      for (int k = 0; k < H; ++k) {
+        fp[k] = fc[k];
+        fc[k] = fn[k];
+      }
     }
     if (!(pmin > 0.0 && pmin <= DBL_MAX)) st |= MTG_TRAJ_NOT_SPD;
 
-    // backward substitution: y_v = z_v - G_v y_{v+1}
-    for (int v = K - 1; v >= 0; --v) {
-      const double* Gv = G + (size_t)v * H * H;
-      for (int d = 0; d < D; ++d) {
-        double* y = Z + ((size_t)v * D + d) * H;
-        const double* yn = Z + ((size_t)(v + 1) * D + d) * H;
-        for (int i = 0; i < H; ++i) {
-          double t = y[i];
-          for (int c = 0; c < H; ++c) t -= Gv[i * H + c] * yn[c];
-          y[i] = t;
+    // backward substitution: y_v = z_v - G_v y_{v+1} (free entries), then the full layout with the
+    // pinned entries 0, vertex by vertex from the end (y_{v+1} is still compressed when y_v needs it)
+    {
+      expand(Z + (size_t)K * D * H, D, mask[K] & HM);
+      for (int v = K - 1; v >= 0; --v) {
+        const unsigned mvv = mask[v] & HM, mnx = mask[v + 1] & HM;
+        const int ncv = H - __builtin_popcount(mvv);
+        const double* Gv = G + (size_t)v * H * H;
+        int fnx[H], nnx = 0;
+        for (int k = 0; k < H; ++k)
+          if (!((mnx >> k) & 1u)) fnx[nnx++] = k;
+        for (int d = 0; d < D; ++d) {
+          double* y = Z + ((size_t)v * D + d) * H;
+          const double* yn = Z + ((size_t)(v + 1) * D + d) * H;  // (already expanded)
+          for (int i = 0; i < ncv; ++i) {
+            double t = y[i];
+            for (int c = 0; c < nnx; ++c) t -= Gv[i * H + c] * yn[fnx[c]];
+            y[i] = t;
+          }
         }
+        expand(Z + (size_t)v * D * H, D, mvv);
       }
     }
 
