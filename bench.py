@@ -253,12 +253,33 @@ def self_launch(n, argv, cmd=None, popen=None):
     return rc
 
 
-def make_problems(workload, N, K, B, seed0):
+PATTERNS = {
+    "generator": "the reference generators' vertex pattern (ends fix derivatives 0..4, interior vertices "
+                 "their position)",
+    "accel-ends": "off-pattern: createRandomVertices(ACCELERATION, K, [-50]^3, [50]^3, seed) + "
+                  "estimateSegmentTimes(3, 5): ends fix derivatives 0..2 only (the reference's "
+                  "2_vertices_rand pattern, test/test_polynomial_optimization.cpp:747-774)",
+    "interior-vel": "off-pattern: the workload's problems with every interior vertex also fixing its "
+                    "velocity (to 0: a stop-and-go waypoint path)",
+}
+
+
+def make_problems(workload, N, K, B, seed0, pattern="generator"):
     import mav_trajectory_generation_cmake_amd as mtg
+    if pattern == "accel-ends":
+        return mtg.random_vertices_batch(N, 3, K, B, [-50.0] * 3, [50.0] * 3, seed0=seed0, max_derivative=2,
+                                         v_max=3.0, a_max=5.0)
     if workload == "config4":
-        return mtg.random_vertices_batch(N, 3, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=seed0,
-                                         max_derivative=4, v_max=3.0, a_max=5.0)
-    return mtg.random_vertices_path_batch(N, 3, K, B, seed0=seed0)
+        values, mask, times = mtg.random_vertices_batch(N, 3, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0],
+                                                        seed0=seed0, max_derivative=4, v_max=3.0, a_max=5.0)
+    else:
+        values, mask, times = mtg.random_vertices_path_batch(N, 3, K, B, seed0=seed0)
+    if pattern == "interior-vel":
+        mask = mask.copy()
+        mask[:, 1:-1] |= 2
+        values = values.copy()
+        values[:, 1:-1, 1, :] = 0.0
+    return values, mask, times
 
 
 def main():
@@ -273,6 +294,8 @@ def main():
                          "GPU clocks settle over ~100 ms of back-to-back launches)")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2")
     ap.add_argument("--batch", type=int, default=10000, help="trajectories per GPU (configs 2, 4, 5: 1e4)")
+    ap.add_argument("--pattern", choices=sorted(PATTERNS), default="generator",
+                    help="vertex constraint pattern of the solve workloads (off-pattern A/B; not the headline)")
     ap.add_argument("--segments", type=int, default=None)
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--timing-stride", type=int, default=0,
@@ -281,6 +304,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample", type=int, default=20000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true",
+                    help="skip the host-array leg (profiling runs: the trace then holds only the bench's own grid)")
     ap.add_argument("--split", action="store_true", help="two-kernel path (assembly + block Cholesky)")
     ap.add_argument("--general-kernel", action="store_true",
                     help="force the general LDS-resident fused kernel (A/B against the default)")
@@ -322,7 +347,7 @@ def main():
         N, K, r = args.N or 10, args.segments or 10, 4
     D = 3
     B = args.batch
-    values, mask, times = make_problems(wl, N, K, B, shard_seed0(rank, B))
+    values, mask, times = make_problems(wl, N, K, B, shard_seed0(rank, B), args.pattern)
     v_d = torch.from_numpy(values).to(dev)
     m_d = torch.from_numpy(mask).to(dev)
     t_d = torch.from_numpy(times).to(dev)
@@ -429,6 +454,9 @@ def main():
             data = ("synthetic: reference bench generator createRandomVerticesPath(3,10,5.0,SNAP,seed) "
                     "+ estimateSegmentTimes(2,2,6.5), seeds rank*B..rank*B+B-1")
         unit = "trajectories/s"
+        if args.pattern != "generator":
+            workload += "; pattern %s" % args.pattern
+            data = "synthetic, " + PATTERNS[args.pattern]
     total = units * world * args.steps
     value = total / el
     achieved = bpt * B / (kern_ms * 1e-3) / 1e9
@@ -464,7 +492,7 @@ def main():
     }
     # end-to-end (not `value`): host arrays in and out through the C ABI's staging -- H2D, kernel,
     # D2H, synchronize -- the PCIe-inclusive rate of a caller that holds its batch in host memory
-    if wl != "config5":
+    if wl != "config5" and not args.no_end_to_end:
         out["end_to_end"] = end_to_end(ctx, N, r, values, mask, times, unit, bpt - K * D * N * 8, K * D * N * 8)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # (the CPU baseline is an N = 1 figure)
         host = host_cpu_info()

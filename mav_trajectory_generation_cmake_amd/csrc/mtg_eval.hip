@@ -234,24 +234,18 @@ struct Clock {
   }
 };
 
-__global__ void eval_count_kernel(int K, int64_t B, const double* times, double t_start, double t_end,
-                                  double dt, int64_t* counts) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  Clock ck;
-  ck.init(times + b * K, K, t_start, t_end, dt);
-  Run r;
-  while (ck.next(&r)) {
-  }
-  counts[b] = ck.n;
-}
-
-// A run as stored in the HBM run table (eval_runs_kernel -> eval_range_kernel), 80 B.
+// A run as stored in the HBM run table (eval_runs_kernel -> eval_range_kernel), 64 B.  Its length is
+// the next run's n0 less its own (the last stored run ends at RunHead::n); segs = 2 seg + single.
+// The tin lane of eval_runs_kernel's lane pair writes bytes 0-31 and 56-63, the acc lane 32-55.
 struct RunRec {
-  int64_t n0, L, tm, ti, am, ai;
-  double tin0, acc0;
-  int32_t tE, aE, seg, single;
+  int64_t n0, tm, ti;
+  double tin0;
+  int64_t am, ai;
+  double acc0;
+  int32_t segs;
+  int16_t tE, aE;
 };
+static_assert(sizeof(RunRec) == 64, "RunRec is one 64-B scalar load");
 
 // Per trajectory: how many runs the table holds and, when the clock had not stopped by then, its
 // state after them (the eval wave resumes the clock there).
@@ -261,70 +255,182 @@ struct RunHead {
   int32_t seg, done;
 };
 
-// The clock, one thread per trajectory, writing its first `cap` runs to the run table.  The clock
-// is a serial chain per trajectory; run here, 64 trajectories share a wave's lanes, where the eval
-// kernel's lane 0 would run it alone while its wave waits.  (16 or 32 trajectories per wave, i.e.
-// 4x / 2x the waves, measured slower: count 0.155 -> 0.205 / 0.166 ms at 1e4, scripts/eval_ab_env.sh.)
+// The other lane of a lane pair (2i, 2i + 1): DPP quad_perm [1, 0, 3, 2], no LDS.
+__device__ __forceinline__ int pair_swap(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int64_t pair_swap(int64_t v) {
+  const int lo = pair_swap((int)(uint32_t)v), hi = pair_swap((int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double pair_swap(double v) {
+  return __builtin_bit_cast(double, pair_swap(__builtin_bit_cast(int64_t, v)));
+}
+
+// The reference's clock on a lane pair: the even lane carries tin (and the segment), the odd lane
+// acc.  A run's two progressions and their limits -- tin's binade and T_i, acc's binade and t_end
+// -- are each one lane's work, and the lanes exchange only whether they have a progression and
+// their limit (DPP), so a run's serial chain is half of Clock::next's.  The clock is the run
+// kernels' critical path: one trajectory's ~110 runs back to back, one wave per SIMD.  Every
+// shuffle is executed by both lanes of a pair (a pair stops together).
+struct PairClock {
+  const double* T;
+  int K;
+  double dt, t_end;
+  double x;   // tin (even lane) or acc (odd lane)
+  double Ti;  // (even lane)
+  int seg;    // (even lane)
+  int64_t n;
+  bool done, odd;
+
+  // the reference's checks before a sample (Clock::settle): the odd lane tests acc < t_end, then
+  // the even lane switches segments while tin > T_i
+  __device__ __forceinline__ void settle() {
+    // (each pair_swap is evaluated unconditionally: a lane that skipped it would leave its partner
+    // reading an inactive lane, and the pair would fall out of step)
+    bool stop = done || (odd && !(x < t_end));
+    const bool other = pair_swap((int)stop) != 0;
+    stop = stop || other;
+    if (!stop && !odd) {
+      while (x > Ti) {
+        x = x - Ti;
+        if (++seg >= K) {
+          stop = true;
+          break;
+        }
+        Ti = T[seg];
+      }
+    }
+    const bool other2 = pair_swap((int)stop) != 0;
+    done = stop || other2;
+  }
+
+  __device__ __forceinline__ void init(const double* tms, int K_, double t_start, double t_end_, double dt_, bool odd_,
+                                       bool valid) {
+    T = tms;
+    K = K_;
+    dt = dt_;
+    t_end = t_end_;
+    odd = odd_;
+    n = 0;
+    double acc = 0.0, tin = 0.0;
+    seg = 0;
+    done = !(valid && range_start(tms, K, t_start, &seg, &acc, &tin));
+    x = odd ? acc : tin;
+    Ti = done ? 0.0 : T[seg];
+    settle();
+  }
+
+  // the next run, written to *w (this lane's half) if w; false when the clock has stopped
+  __device__ __forceinline__ bool next(RunRec* w) {
+    if (done) return false;
+    const int64_t n0 = n;
+    const double x0 = x;
+    const int seg0 = seg;
+    Prog p;
+    const bool ok = progression(x, dt, &p);
+    int64_t lim = kNoLimit;
+    if (ok) {
+      const double y = recip(p.inc);
+      lim = floor_div_r(kTwo53 - 1 - p.m, p.inc, y) + 1;  // the binade
+      if (!odd) {
+        lim = min(lim, run_len_le_r(p, __builtin_amdgcn_ldexp(Ti, -p.E), y));  // tin <= T_i
+      } else {
+        const double q = __builtin_amdgcn_ldexp(t_end, -p.E);  // acc < t_end
+        if (q < 4.0e18) lim = min(lim, run_len_le_r(p, __builtin_ceil(q) - 1.0, y));
+      }
+    }
+    const bool both = pair_swap((int)ok) != 0 && ok;
+    const int64_t lim2 = pair_swap(lim);
+    int64_t L = 1;
+    if (both) {
+      const int64_t m = min(lim, lim2);
+      L = m < 1 ? 1 : m;
+      if (L > 1) x = prog_value(p, L - 1);  // the run's last sample, exactly
+    }
+    n += L;
+    x += dt;  // the step after it, as the reference takes it
+    settle();
+    if (w) {
+      if (!odd) {
+        w->n0 = n0;
+        w->tm = p.m;
+        w->ti = p.inc;
+        w->tin0 = x0;
+        w->segs = 2 * seg0 + (both ? 0 : 1);
+        w->tE = (int16_t)p.E;
+      } else {
+        w->am = p.m;
+        w->ai = p.inc;
+        w->acc0 = x0;
+        w->aE = (int16_t)p.E;
+      }
+    }
+    return true;
+  }
+};
+
+// Trajectories per block (one wave) of the clock kernels: a lane pair each.
+constexpr int kPairTraj = 32;
+
+__global__ __launch_bounds__(64) void eval_count_kernel(int K, int64_t B, const double* times, double t_start,
+                                                        double t_end, double dt, int64_t* counts) {
+  const int lane = threadIdx.x;
+  const int64_t b = (int64_t)blockIdx.x * kPairTraj + (lane >> 1);
+  const bool valid = b < B;
+  PairClock ck;
+  ck.init(times + (valid ? b : 0) * K, K, t_start, t_end, dt, lane & 1, valid);
+  while (ck.next(nullptr)) {
+  }
+  if (valid && !(lane & 1)) counts[b] = ck.n;
+}
+
+// The clock, a lane pair per trajectory, writing its first `cap` runs to the run table.  The clock
+// is a serial chain per trajectory; run here, 32 trajectories share a wave, where the eval kernel's
+// lane 0 would run it alone while its wave waits.  (Round 3 ran one lane per trajectory: the run
+// arithmetic of both progressions on one lane, 0.143 ms at 1e4.  16 or 32 trajectories per wave
+// with one lane each measured slower than 64: 0.155 -> 0.205 / 0.166 ms.)
 //
 // With `counts` (the one-call evaluateRange, mtg_evaluate_range_batch_full) the kernel also finishes
 // each clock to get the trajectory's sample count -- the count kernel's work, without running the
-// clock twice -- and, per 64-trajectory block (one wave), writes the exclusive prefix sum of the
+// clock twice -- and, per 32-trajectory block (one wave), writes the exclusive prefix sum of the
 // counts inside the block to offs[b] and the block's total to bsum[block]: the first level of the
 // device-side offsets (eval_scan_kernel, then the eval kernel adds the block's offset).
 __global__ __launch_bounds__(64) void eval_runs_kernel(int K, int64_t B, const double* times, double t_start,
                                                        double t_end, double dt, int cap, RunHead* heads, RunRec* runs,
                                                        int64_t* counts, int64_t* offs, int64_t* bsum) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B && !counts) return;
-  int64_t cnt = 0;
-  if (b < B) {
-  Clock ck;
-  ck.init(times + b * K, K, t_start, t_end, dt);
-  RunRec* rr = runs + b * (int64_t)cap;
+  const int lane = threadIdx.x;
+  const bool odd = lane & 1;
+  const int64_t b = (int64_t)blockIdx.x * kPairTraj + (lane >> 1);
+  const bool valid = b < B;
+  PairClock ck;
+  ck.init(times + (valid ? b : 0) * K, K, t_start, t_end, dt, odd, valid);
+  RunRec* rr = runs + (valid ? b : 0) * (int64_t)cap;
   int64_t nr = 0;
-  Run r;
-  while (nr < cap && ck.next(&r)) {
-    RunRec w;
-    w.n0 = r.n0;
-    w.L = r.L;
-    w.tm = r.t.m;
-    w.ti = r.t.inc;
-    w.am = r.a.m;
-    w.ai = r.a.inc;
-    w.tin0 = r.tin0;
-    w.acc0 = r.acc0;
-    w.tE = r.t.E;
-    w.aE = r.a.E;
-    w.seg = r.seg;
-    w.single = r.single;
-    rr[nr++] = w;
-  }
-  RunHead h;
-  h.nruns = nr;
-  h.n = ck.n;
-  h.acc = ck.acc;
-  h.tin = ck.tin;
-  h.Ti = ck.Ti;
-  h.seg = ck.seg;
-  h.done = ck.done;
-  heads[b] = h;
-  if (counts) {
-    while (ck.next(&r)) {  // the rest of a clock longer than the table: counted only
-    }
-    cnt = ck.n;
-    counts[b] = cnt;
-  }
+  while (nr < cap && ck.next(rr + nr)) ++nr;
+  const double acc = pair_swap(ck.x);  // (the even lane's head needs acc)
+  if (valid && !odd) {
+    RunHead h;
+    h.nruns = nr;
+    h.n = ck.n;
+    h.acc = acc;
+    h.tin = ck.x;
+    h.Ti = ck.Ti;
+    h.seg = ck.seg;
+    h.done = ck.done;
+    heads[b] = h;
   }
   if (!counts) return;
-  // exclusive prefix of the wave's counts (lanes past B count 0) and the block total
-  const int lane = threadIdx.x;
+  while (ck.next(nullptr)) {  // the rest of a clock longer than the table: counted only
+  }
+  const int64_t cnt = valid && !odd ? ck.n : 0;
+  if (valid && !odd) counts[b] = cnt;
+  // exclusive prefix of the wave's counts (odd lanes and lanes past B count 0) and the block total
   int64_t incl = cnt;
 #pragma unroll
   for (int m = 1; m < 64; m <<= 1) {
     const int64_t o = __shfl_up(incl, m, 64);
     if (lane >= m) incl += o;
   }
-  if (b < B) offs[b] = incl - cnt;
+  if (valid && !odd) offs[b] = incl - cnt;
   if (lane == 63) bsum[blockIdx.x] = incl;
 }
 
@@ -356,11 +462,14 @@ __global__ __launch_bounds__(kScanThreads) void eval_scan_kernel(int64_t nb, int
 }
 
 // Runs per round of the LDS table (from the run table, or built by lane 0), consumed by the wave.
-constexpr int kRuns = 64;
+#ifndef MTG_EVAL_RUNS
+#define MTG_EVAL_RUNS 32
+#endif
+constexpr int kRuns = MTG_EVAL_RUNS;
 constexpr int kEvalThreads = 64;
 
 // (A run's length is the next run's n0 less its own.  Config 2, K = 10, D = 3, N = 10: this table
-// 4.6 KB + the Horner terms 2.4 KB + the staged block 3 KB = 10 KB per wave, so 16 waves -- 4 per
+// 2.3 KB + the Horner terms 2.4 KB + the staged block 3 KB = 7.7 KB per wave, so 20 waves -- 5 per
 // SIMD, amdgpu_waves_per_eu below -- fit in a CU's 160 KB.)
 struct RunLds {  // structure of arrays in LDS
   int64_t n0[kRuns], tm[kRuns], ti[kRuns], am[kRuns], ai[kRuns];
@@ -368,27 +477,37 @@ struct RunLds {  // structure of arrays in LDS
   int tE[kRuns], aE[kRuns], seg[kRuns], single[kRuns];
 };
 
+// Whether a trajectory is eval_range_kernel<..., ST = true>'s: its whole clock is in the run table
+// (the run kernel finished it) and its rows are addressable with 32-bit byte offsets.
+__device__ __forceinline__ bool stored_whole(const RunHead& h, int64_t n_total, int D) {
+  return h.done != 0 && n_total * (int64_t)(D * 8) < (int64_t)kBufOOB;
+}
+
 // One wave per trajectory: lane 0 turns the clock into runs (a few tens per segment), all lanes
 // evaluate the runs' samples -- consecutive samples on consecutive lanes -- with the coefficients
 // staged in LDS.
 // DER >= 0: the derivative order at compile time (0..4, the common ones); DER < 0: `derivative`.
 // DD > 0: D at compile time (the sample loop takes kSpl samples per lane per block); 0: D at run time.
+// ST: only the trajectories whose whole clock is in the run table (stored_whole), with the D = DD
+// sample loop alone: no clock on lane 0 and no run-time-D loop in the kernel, which leaves it the
+// registers of the sample loop only (the one-call evaluateRange; a second launch, ST = false with
+// `rest`, takes the others).
 constexpr int kSpl = 2;
 #ifndef MTG_EVAL_EXP
 #define MTG_EVAL_EXP 0  // (diagnostic builds only: 1 no run lookup, 2 no Horner, 3 stores dropped)
 #endif
 #ifndef MTG_EVAL_WAVES
-#define MTG_EVAL_WAVES 4
+#define MTG_EVAL_WAVES 5
 #endif
-template <int N, int DER, int DD>
-__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MTG_EVAL_WAVES))) void eval_range_kernel(int D, int K, const double* coeffs,
+template <int N, int DER, int DD, bool ST>
+__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST ? MTG_EVAL_WAVES : 4))) void eval_range_kernel(int D, int K, const double* coeffs,
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
                                                                   double* sample_times, int cap,
                                                                   const RunHead* heads, const RunRec* runs,
                                                                   const int64_t* boff, int64_t* offsets_out,
-                                                                  int64_t capacity, const int64_t* total) {
+                                                                  int64_t capacity, const int64_t* total, bool rest) {
   // HIP defaults to -ffp-contract=fast-honor-pragmas: without this pragma the Horner step below
   // becomes an FMA (v_fmac_f64) and differs from the reference in the last bit.
 #pragma clang fp contract(off)
@@ -396,8 +515,13 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   const int64_t n_total = counts[b];
+  if constexpr (ST) {
+    if (!stored_whole(heads[b], n_total, D)) return;
+  } else {
+    if (rest && stored_whole(heads[b], n_total, D)) return;  // (the ST launch has taken it)
+  }
   // offsets: given (offsets[b]), or device-side (the in-block prefix offsets[b] + the block's offset)
-  const int64_t base = boff ? offsets[b] + boff[b >> 6] : offsets[b];
+  const int64_t base = boff ? offsets[b] + boff[b / kPairTraj] : offsets[b];
   if (boff && lane == 0) offsets_out[b] = base;
   // (past the caller's capacity -- this trajectory's rows, or the call's total when it is known on the
   // device: then nothing at all is written)
@@ -408,7 +532,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
   // The D-at-compile-time sample loop stores through buffer resources over this trajectory's rows and
   // sample times, addressed by 32-bit byte offsets (a trajectory with under 2 GiB of rows; longer
   // ones take the run-time-D loop), with 16-B pieces when `out` is 16-B aligned.
-  const bool fast = DD > 0 && n_total * (int64_t)(D * 8) < (int64_t)kBufOOB;
+  const bool fast = ST || (DD > 0 && n_total * (int64_t)(D * 8) < (int64_t)kBufOOB);
   const bool al16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
   const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out + base * D, fast ? (uint32_t)(n_total * D * 8) : 0u);
   const __amdgpu_buffer_rsrc_t rs =
@@ -420,12 +544,13 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
   // per-sample products
   for (int i = lane; i < K * D * N; i += kEvalThreads) cf[i] = base_coeff(derivative, i % N) * cb[i];
   Clock ck;
-  int64_t stored = 0, next_run = 0;  // runs in the HBM table, runs taken from it
+  int64_t stored = 0, next_run = 0, stored_end = 0;  // runs in the HBM table, runs taken from it, where they end
   const RunRec* rr = runs ? runs + b * (int64_t)cap : nullptr;
   if (heads) {
     const RunHead h = heads[b];
     stored = h.nruns;
-    if (lane == 0) {  // resume the clock after the stored runs
+    stored_end = h.n;
+    if (!ST && lane == 0) {  // resume the clock after the stored runs
       ck.T = times + b * K;
       ck.K = K;
       ck.dt = dt;
@@ -437,7 +562,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
       ck.n = h.n;
       ck.done = h.done != 0;
     }
-  } else if (lane == 0) {
+  } else if (!ST && lane == 0) {
     ck.init(times + b * K, K, t_start, t_end, dt);
   }
   __shared__ int s_nr;
@@ -456,12 +581,14 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
         rt->aE[lane] = w.aE;
         rt->tin0[lane] = w.tin0;
         rt->acc0[lane] = w.acc0;
-        rt->seg[lane] = w.seg;
-        rt->single[lane] = w.single;
-        if (lane == nr - 1) s_end = w.n0 + w.L;
+        rt->seg[lane] = w.segs >> 1;
+        rt->single[lane] = w.segs & 1;
+        if (lane == nr - 1) s_end = next_run + nr < stored ? rr[next_run + nr].n0 : stored_end;
       }
       if (lane == 0) s_nr = nr;
       next_run += nr;
+    } else if (ST) {
+      if (lane == 0) s_nr = 0;  // (the table held the whole clock)
     } else if (lane == 0) {
       int nr = 0;
       Run r;
@@ -487,7 +614,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(MT
     if (nr == 0) break;
     const int64_t first = rt->n0[0], end = s_end < n_total ? s_end : n_total;
     int ri = 0;
-    if (DD > 0 && fast) {
+    if (ST || (DD > 0 && fast)) {
       // D at compile time: each lane takes kSpl samples per block (n = nb + s 64 + lane), and their
       // kSpl D Horner chains are independent, so they interleave instead of running one dimension
       // after the other; the staged rows are read back in one batch before the stores.
@@ -682,11 +809,12 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
                              double t_end, double dt, int64_t* counts, hipStream_t stream) {
   (void)N;
   (void)D;
-  const int block = 64;  // (256-thread blocks put the 1e4 clocks of config 2 on 40 CUs: 0.163 -> 0.154 ms)
-  const int64_t grid = (B + block - 1) / block;
+  // one wave per 32 trajectories (a lane pair each); (256-thread blocks put the 1e4 clocks of config
+  // 2 on 40 CUs: 0.163 -> 0.154 ms, round 2)
+  const int64_t grid = (B + kPairTraj - 1) / kPairTraj;
   if (grid == 0) return hipSuccess;
-  launch_kernel(eval_count_kernel, dim3((unsigned)grid), dim3(block), 0, stream, K, B, times, t_start,
-                     t_end, dt, counts);
+  launch_kernel(eval_count_kernel, dim3((unsigned)grid), dim3(64), 0, stream, K, B, times, t_start, t_end, dt,
+                counts);
   return hipGetLastError();
 }
 
@@ -704,7 +832,7 @@ size_t eval_workspace_bytes(int K, int64_t B, int* cap) {
 
 size_t eval_full_workspace_bytes(int K, int64_t B, int* cap) {
   // the run table, then the per-block totals and the grand total
-  return eval_workspace_bytes(K, B, cap) + sizeof(int64_t) * (size_t)((B + 63) / 64 + 1);
+  return eval_workspace_bytes(K, B, cap) + sizeof(int64_t) * (size_t)((B + kPairTraj - 1) / kPairTraj + 1);
 }
 
 hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double t_start, double t_end, double dt,
@@ -714,7 +842,7 @@ hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double
   RunHead* heads = static_cast<RunHead*>(ws);
   RunRec* runs = reinterpret_cast<RunRec*>(heads + B);
   int64_t* bsum = reinterpret_cast<int64_t*>(runs + (size_t)B * cap);
-  const int64_t nb = (B + 63) / 64;
+  const int64_t nb = (B + kPairTraj - 1) / kPairTraj;
   launch_kernel(eval_runs_kernel, dim3((unsigned)nb), dim3(64), 0, stream, K, B, times, t_start, t_end, dt, cap,
                 heads, runs, counts, offsets, bsum);
   hipLaunchKernelGGL(eval_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, nb, bsum, total);
@@ -736,8 +864,7 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
     if (runs_ready) {  // launch_eval_runs_counts filled the table, the in-block offsets and the block offsets
       boff = reinterpret_cast<const int64_t*>(runs + (size_t)B * cap);
     } else {
-      const int block = 64;
-      launch_kernel(eval_runs_kernel, dim3((unsigned)((B + block - 1) / block)), dim3(block), 0, stream, K, B, times,
+      launch_kernel(eval_runs_kernel, dim3((unsigned)((B + kPairTraj - 1) / kPairTraj)), dim3(64), 0, stream, K, B, times,
                     t_start, t_end, dt, cap, heads, runs, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
     }
   }
@@ -749,16 +876,30 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)(d3 ? kSpl : 1) * kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   const dim3 grid((unsigned)B);
+  // D = 3 with the run table: an ST launch takes every trajectory whose whole clock is in it, and
+  // the run-time-D kernel (rest) the others -- its blocks for the stored ones return at once
+#ifndef MTG_EVAL_STORED
+#define MTG_EVAL_STORED 1  // (0: one launch of the D = 3 kernel with the lane-0 clock, for A/B builds)
+#endif
+  const bool stored = MTG_EVAL_STORED && heads != nullptr && d3;
 #define MTG_EVAL_LAUNCH(NN, DER)                                                                                   \
   do {                                                                                                             \
-    if (d3)                                                                                                        \
-      launch_kernel(eval_range_kernel<NN, DER, 3>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
-                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
-                    offsets_out, capacity, total);                                                                 \
-    else                                                                                                           \
-      launch_kernel(eval_range_kernel<NN, DER, 0>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs, times,     \
-                    t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs, boff,   \
-                    offsets_out, capacity, total);                                                                 \
+    if (stored) {                                                                                                  \
+      launch_kernel(eval_range_kernel<NN, DER, 3, true>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,      \
+                    times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
+                    boff, offsets_out, capacity, total, false);                                                    \
+      launch_kernel(eval_range_kernel<NN, DER, 0, false>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,     \
+                    times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
+                    boff, offsets_out, capacity, total, true);                                                     \
+    } else if (d3) {                                                                                               \
+      launch_kernel(eval_range_kernel<NN, DER, 3, false>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,     \
+                    times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
+                    boff, offsets_out, capacity, total, false);                                                    \
+    } else {                                                                                                       \
+      launch_kernel(eval_range_kernel<NN, DER, 0, false>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,     \
+                    times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
+                    boff, offsets_out, capacity, total, false);                                                    \
+    }                                                                                                              \
   } while (0)
 #define MTG_EVAL_CASE(NN)                 \
   case NN:                                \

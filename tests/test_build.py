@@ -33,8 +33,9 @@ def test_evaluate_range_has_no_fma(tmp_path):
     """Polynomial::evaluate (polynomial.h:138-151) multiplies then adds; an FMA would change the
     last bit and break bit-exact parity of evaluateRange with the reference."""
     bodies = _kernel_bodies(_device_asm("mtg_eval.hip", tmp_path), r"_ZN3mtg17eval_range_kernel")
-    # N = 2, 4, ..., 12 x derivative 0..4 and the runtime-derivative variant x D = 3 / run-time D
-    assert len(bodies) == 72
+    # N = 2, 4, ..., 12 x derivative 0..4 and the runtime-derivative variant x (D = 3, D = 3 stored-run
+    # only (ST), run-time D)
+    assert len(bodies) == 108
     for name, body in bodies.items():
         # f64 FMAs are allowed only as the compiler's f64 -> int64 conversion idiom (x - 2^32 hi,
         # constant 0xc1f00000) in the clock's integer run arithmetic; f32 FMAs belong to its
