@@ -74,29 +74,37 @@ extern "C" {
 #define MTG_FLAG_SPLIT_KERNELS 4u      /* two-kernel path: assembly kernel + block-Cholesky kernel */
 #define MTG_FLAG_GENERAL_KERNEL 8u     /* diagnostics: always use the general LDS-resident fused kernel
                                           (default: see mtg_solve_kernel) */
-/* (16u and 32u selected the lane-per-chain and interior-waypoint lane kernels, retired in round 4:
- * measured slower than the default everywhere, DESIGN.md 3.2.  The bits are reserved and ignored.) */
+/* Deprecated (ABI 1 names kept so round-3 callers still compile): 16u and 32u selected the
+ * lane-per-chain and interior-waypoint lane kernels, retired in round 4 (measured slower than the
+ * default everywhere).  The bits are reserved and ignored: a call that sets them runs
+ * the default kernel, and mtg_solve_kernel never returns MTG_KERNEL_LANE or MTG_KERNEL_IP. */
+#define MTG_FLAG_LANE_KERNEL 16u       /* deprecated, ignored */
+#define MTG_FLAG_IP_KERNEL 32u         /* deprecated, ignored */
 
-#define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10, K = 10, D <= 4, r >= 1;
-                                          one lane per (chain, dimension); trajectories whose masks are not
-                                          the reference generators' pattern are solved by the general fused
-                                          kernel's block function inside it, with the general kernel's
-                                          bits): DESIGN.md 3.2c.  The default for those shapes at every
-                                          batch size */
+#define MTG_FLAG_DL_KERNEL 64u         /* the dimension-lane kernel where it applies (N = 10 with K = 10,
+                                          N = 12 with K = 20; D <= 4, r >= 1; one lane per (chain,
+                                          dimension)).  The reference generators' pattern takes its pattern
+                                          pass, any other mask with every position fixed its general-mask
+                                          pass, and a trajectory with a free position the general fused
+                                          kernel's block function inside it (with that kernel's bits):
+                                          DESIGN.md 3.2c.  The default for those shapes at every batch size */
 #define MTG_FLAG_COLUMN_KERNEL 128u    /* the register column kernel wherever it applies, also where the
                                           default for the batch size is the dimension-lane kernel (A/B) */
-#define MTG_DL_MIN_BATCH 1             /* (round 3: 2048.)  Since round 4 the dimension-lane kernel is the
+#define MTG_DL_MIN_BATCH 1             /* Deprecated (round 3: 2048; kept as 1 for callers that test it).
+                                          Since round 4 the dimension-lane kernel is the
                                           default at every batch size where it applies, so a trajectory's
                                           result never depends on the size of the call or on the other
                                           trajectories in it (it was faster at every size) */
 
-/* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape. */
+/* Solve kernels (mtg_solve_kernel): which one mtg_solve_linear_batch runs for a shape.  (1 and 5,
+   MTG_KERNEL_LANE and MTG_KERNEL_IP, named the kernels retired in round 4: deprecated, never returned.) */
+#define MTG_KERNEL_LANE 1              /* deprecated */
+#define MTG_KERNEL_IP 5                /* deprecated */
 #define MTG_KERNEL_COLUMN 2            /* default: register column kernel, a lane per column of G_v /
                                           per dimension, twisted (K <= 12, N = 12 up to K = 20) */
 #define MTG_KERNEL_GENERAL 3           /* general LDS-resident fused kernel (any K) */
 #define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
-#define MTG_KERNEL_DL 6                /* one lane per (chain, dimension), interior-waypoint pattern
-                                          (MTG_FLAG_DL_KERNEL) */
+#define MTG_KERNEL_DL 6                /* one lane per (chain, dimension) (MTG_FLAG_DL_KERNEL) */
 
 typedef struct mtg_ctx mtg_ctx;
 

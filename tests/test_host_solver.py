@@ -195,3 +195,27 @@ def test_host_min_max_magnitude_vs_oracle(derivative, dims):
             assert abs(got["value"] - ref[1]) <= 1e-9 * scale, (b, got, ref)
             if got["segment"] == ref[2]:
                 assert abs(got["time"] - ref[0]) <= 1e-6 * times[b, ref[2]] or abs(got["value"] - ref[1]) <= 1e-12 * scale
+
+
+def test_host_solve_bitwise_fixture():
+    """The host solve against its own earlier full-layout sweep, bit for bit: round 4
+    restricted the forward and backward sweeps to each vertex's free derivatives, claimed bit-identical
+    because the pinned rows and columns only added exact zeros.  tests/golden/make_host_fixture.py
+    built the pre-change mtg_host_solve.cpp (commit 46c85dc) and recorded its coefficients, free
+    values, n_free, cost and status on fully pinned / fully free vertices, free end derivatives, random
+    pins and free positions, for 7 shapes."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "host_solve_bitwise.npz"))
+    keys = sorted({k.split("__")[0] for k in g.files if "__" in k})
+    assert len(keys) == 7
+    for key in keys:
+        N, D, K, r = (int(x[1:]) for x in key.split("_"))
+        vals, mask, times = g[key + "__values"], g[key + "__mask"], g[key + "__times"]
+        out = mtg.host_solve_linear_batch(N, r, vals, mask, times, free=True, n_free=True, cost=True, status=True)
+        nf = g[key + "__n_free"]
+        np.testing.assert_array_equal(out["coeffs"], g[key + "__coeffs"], err_msg=key)
+        np.testing.assert_array_equal(out["n_free"], nf, err_msg=key)
+        for b in range(len(nf)):
+            np.testing.assert_array_equal(out["free"][b, :, :nf[b]], g[key + "__free"][b, :, :nf[b]], err_msg=key)
+        np.testing.assert_array_equal(out["cost"], g[key + "__cost"], err_msg=key)
+        np.testing.assert_array_equal(out["status"], g[key + "__status"], err_msg=key)

@@ -128,3 +128,47 @@ def test_host_default_threads_respect_affinity_and_quota():
             assert n <= max(1, int(float(q) / float(p)))
     except OSError:
         pass
+
+
+_CG_DRIVER = r"""
+#include "mtg_host_threads.h"
+#include <cstdio>
+#include <string>
+int main(int argc, char** argv) {
+  std::string pc;
+  for (const char* p = argv[3]; *p; ++p) pc += (*p == ';') ? '\n' : *p;
+  std::printf("%d\n", mtg::cgroup_quota_cpus(argv[1], argv[2], pc));
+  return 0;
+}
+"""
+
+
+def test_cgroup_quota_walks_ancestors_and_v1(tmp_path):
+    """mtg::cgroup_quota_cpus (ADVICE r4): the tightest quota over the process's cgroup and every
+    ancestor (a quota on a parent cgroup, or a nested cgroup without a cgroup namespace), and the v1
+    cpu.cfs_quota_us / cpu.cfs_period_us files; "max" and -1 mean no quota."""
+    src = tmp_path / "cg.cpp"
+    src.write_text(_CG_DRIVER)
+    exe = tmp_path / "cg"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "mav_trajectory_generation_cmake_amd", "csrc"),
+                    str(src), "-o", str(exe)], check=True)
+    v2 = tmp_path / "v2"
+    v1 = tmp_path / "v1"
+    for d, txt in (("", "max 100000"), ("kube", "1600000 100000"), ("kube/pod", "max 100000"),
+                   ("kube/pod/ctr", "max 100000"), ("loose", "250000 100000")):
+        (v2 / d).mkdir(parents=True, exist_ok=True)
+        (v2 / d / "cpu.max").write_text(txt + "\n")
+    for d, q, p in (("", -1, 100000), ("a", 800000, 100000), ("a/b", -1, 100000)):
+        (v1 / d).mkdir(parents=True, exist_ok=True)
+        (v1 / d / "cpu.cfs_quota_us").write_text("%d\n" % q)
+        (v1 / d / "cpu.cfs_period_us").write_text("%d\n" % p)
+
+    def run(pc):
+        r = subprocess.run([str(exe), str(v2), str(v1), pc], capture_output=True, text=True, check=True)
+        return int(r.stdout)
+    assert run("0::/kube/pod/ctr") == 16          # the parent's quota caps the nested cgroup
+    assert run("0::/loose") == 2                  # its own quota (2.5 CPUs -> 2)
+    assert run("0::/") == 0                       # namespace root without a quota
+    assert run("12:cpu,cpuacct:/a/b;0::/") == 0   # hybrid: the v2 line wins
+    assert run("12:cpu,cpuacct:/a/b") == 8        # v1: the ancestor's cfs quota
+    assert run("3:memory:/x;5:cpuset:/y") == 0    # no cpu controller line
