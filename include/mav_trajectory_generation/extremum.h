@@ -1,4 +1,10 @@
 // extremum.h -- Extremum (reference extremum.h:28-52).
+//
+// The struct, its comparison operators and its operator<< format restate the reference's public
+// interface (mav_trajectory_generation/include/mav_trajectory_generation/extremum.h, Copyright (c)
+// 2016 Markus Achtelik, Michael Burri, Helen Oleynikova, Rik Baehnemann, Marija Popovic, ASL, ETH
+// Zurich; Apache License 2.0, http://www.apache.org/licenses/LICENSE-2.0): the names,
+// fields and output format are the drop-in's contract.
 #ifndef MAV_TRAJECTORY_GENERATION_EXTREMUM_H_
 #define MAV_TRAJECTORY_GENERATION_EXTREMUM_H_
 

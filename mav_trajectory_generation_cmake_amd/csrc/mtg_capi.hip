@@ -483,7 +483,8 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
   // (a time sweep passes scales, also with one candidate: it takes the single-stream path, which stages them)
   if (!(flags & (MTG_FLAG_DEVICE_PTRS | MTG_FLAG_SPLIT_KERNELS)) && n_cand == 1 && !scales &&
       (size_t)batch * (sizeof(double) * ((size_t)V * h * D + K + (size_t)K * D * N) + V) > kPipelineMinBytes) {
-    // the chunks run the kernel the whole batch would (the default depends on the batch size)
+    // the chunks run the kernel the whole batch would (the default is the same at every batch size;
+    // the explicit flag keeps it so)
     const unsigned kf = flags & (MTG_FLAG_GENERAL_KERNEL |
                                  MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
     const unsigned pin = mtg::solve_kernel(N, D, K, kf, r, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
@@ -781,8 +782,9 @@ int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D,
   const int V = K + 1, h = N / 2;
   const size_t s_vals = (size_t)V * h * D, s_coef = (size_t)K * D * N, s_free = (size_t)D * V * h;
   std::vector<int> rcs(n_ctxs, MTG_OK);
-  // every shard runs the kernel the whole batch would on one device (the default depends on the
-  // batch size), so the result does not depend on the number of devices
+  // every shard runs the kernel the whole batch would on one device (the default no longer depends on
+  // the batch size -- the DL kernel for N = 10 / K = 10 and N = 12 / K = 20 at every size -- but the
+  // flag keeps the choice explicit), so the result does not depend on the number of devices
   if (!(flags & MTG_FLAG_SPLIT_KERNELS))
     flags |= mtg::solve_kernel(N, D, K, flags, derivative_to_optimize, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
                                                                                              : MTG_FLAG_COLUMN_KERNEL;

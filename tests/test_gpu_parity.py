@@ -1002,20 +1002,26 @@ def test_dl_kernel_vs_column_and_oracle(gpu_ctx, D, r):
     ref = O.solve_linear_batch(N, r, vals, mask.astype(np.uint32), times)
     assert scale_normalised_error(dl["coeffs"], ref, times) <= 1e-6
     assert check_path(vals, mask, times, dl["coeffs"], N, relative=True) < 1e-6
-    # another pattern: trajectory 2 tpw + 1 fixes a velocity at vertex 2.  It alone is solved by the
-    # general kernel's block function (the fallback), with that kernel's bits; every other trajectory,
-    # its wave-mates included, keeps the bits it had without it (round 4: per trajectory, not per wave)
+    # other patterns: trajectory 2 tpw + 1 fixes a velocity at vertex 2 (the general-mask DL pass:
+    # against the general kernel at 1e-9), trajectory 4 tpw + 2 frees the position of vertex 3 (the
+    # fallback: the general kernel's block function, with that kernel's bits); every other trajectory,
+    # its wave-mates included, keeps the bits it had without them (per trajectory, not per wave)
     m2 = mask.copy()
-    bad = 2 * tpw + 1
+    bad, fb = 2 * tpw + 1, 4 * tpw + 2
     m2[bad, 2] |= 2
+    m2[fb, 3] &= np.uint8(0xFE)
     dl2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, dl=True, **kw)
     col2 = gpu_ctx.solve_linear_batch(N, r, vals, m2, times, general=True, **kw)
-    others = np.arange(B) != bad
+    others = (np.arange(B) != bad) & (np.arange(B) != fb)
+    assert scale_normalised_error(dl2["coeffs"][bad:bad + 1], col2["coeffs"][bad:bad + 1], times[bad:bad + 1]) <= 1e-9
+    np.testing.assert_allclose(dl2["cost"][bad], col2["cost"][bad], rtol=1e-9)
+    for k in ("status", "n_free"):
+        np.testing.assert_array_equal(dl2[k][bad], col2[k][bad], err_msg=k)
     for k in ("coeffs", "cost", "free", "status", "n_free"):
         if k == "cost":  # (the general kernel sums the cost over its 8 or 16 lanes: 1-ulp differences)
-            np.testing.assert_allclose(dl2[k][bad], col2[k][bad], rtol=1e-14, err_msg=k)
+            np.testing.assert_allclose(dl2[k][fb], col2[k][fb], rtol=1e-14, err_msg=k)
         else:
-            np.testing.assert_array_equal(dl2[k][bad], col2[k][bad], err_msg=k)
+            np.testing.assert_array_equal(dl2[k][fb], col2[k][fb], err_msg=k)
         np.testing.assert_array_equal(dl2[k][others], dl[k][others], err_msg=k)
 
 
@@ -1131,8 +1137,8 @@ def test_result_independent_of_batch_composition(gpu_ctx, N, D, K, r):
     wave-mates through the general kernel).  Default path, a batch of 2500 with ~8% of trajectories
     carrying extra fixed interior derivatives (another pattern): the whole batch, the batch reversed,
     chunks of 37 and of 1500, and single trajectories all give the same coefficients, free values,
-    cost and status, bit for bit.  Shapes: config 2 and D = 1 (DL kernel), config 4 (wide column
-    bucket), N = 8 (column kernel), K = 13 (general kernel)."""
+    cost and status, bit for bit.  Shapes: config 2, D = 1 and config 4 (DL kernel: the odd
+    trajectories take its general-mask pass), N = 8 (column kernel), K = 13 (general kernel)."""
     from mav_trajectory_generation_cmake_amd import random_vertices_path_batch
     B = 2500
     vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=7700, max_derivative=min(4, N // 2 - 1))
@@ -1196,3 +1202,111 @@ def test_config4_full_size_dl_vs_column(gpu_ctx):
     nf = int(dl["n_free"][0])
     fs = np.max(np.abs(col["free"][:, :, :nf]), axis=2, keepdims=True)
     assert np.max(np.abs(dl["free"][:, :, :nf] - col["free"][:, :, :nf]) / fs) <= 1e-7
+
+
+def _off_pattern_batch(N, D, K, B, seed0, kind):
+    """Off-pattern masks with every position fixed (the DL kernel's general-mask pass): "random"
+    pins derivatives 1..N/2-1 at random per vertex (values random), "accel" is createRandomVertices
+    with ends fixed to ACCELERATION (the reference's 2_vertices_rand pattern,
+    test/test_polynomial_optimization.cpp:747-774), "vel" adds a fixed velocity at every interior
+    vertex, "mixed" mixes the pattern, both kinds above and a free interior position (fallback)."""
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch, random_vertices_path_batch
+    h = N // 2
+    rng = np.random.default_rng(seed0)
+    if kind == "accel":
+        return random_vertices_batch(N, D, K, B, [-50.0] * D, [50.0] * D, seed0=seed0, max_derivative=min(2, h - 1))
+    vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=seed0, max_derivative=min(4, h - 1))
+    vals, mask = vals.copy(), mask.copy()
+    if kind == "vel":
+        mask[:, 1:-1] |= 2
+        vals[:, 1:-1, 1, :] = rng.normal(size=vals[:, 1:-1, 1, :].shape)
+    elif kind in ("random", "mixed"):
+        sel = rng.random(B) < (1.0 if kind == "random" else 0.5)
+        pins = (rng.integers(0, 1 << h, size=(B, K + 1)) | 1).astype(np.uint8)
+        mask[sel] = pins[sel]
+        vals[sel, :, 1:, :] = rng.normal(size=vals[sel, :, 1:, :].shape)
+        if kind == "mixed":
+            free_pos = rng.random(B) < 0.05
+            mask[free_pos, K // 2] &= np.uint8(0xFE)  # a free interior position: the fallback
+    return vals, mask, times
+
+
+@pytest.mark.parametrize("N,D,K,r,kind", [(10, 3, 10, 4, "random"), (10, 3, 10, 4, "accel"), (10, 3, 10, 4, "vel"),
+                                          (10, 3, 10, 4, "mixed"), (10, 1, 10, 2, "random"), (10, 4, 10, 3, "mixed"),
+                                          (10, 2, 10, 4, "vel"), (12, 3, 20, 3, "random"), (12, 3, 20, 3, "accel"),
+                                          (12, 4, 20, 3, "mixed")])
+def test_dl_general_masks_vs_general_kernel_and_oracle(gpu_ctx, N, D, K, r, kind):
+    """The DL kernel's general-mask pass (round 5): every mask with all positions fixed, solved by the
+    dimension-lane recurrence with runtime pinning, against the general kernel (1e-8 scale-normalised)
+    and the oracle (1e-6), with free values (the reference's (vertex, derivative) order), n_free, cost
+    and status; trajectories with a free position (kind "mixed") go through the fallback."""
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    B = 437  # ragged: not a multiple of the trajectories per wave
+    vals, mask, times = _off_pattern_batch(N, D, K, B, 900 + N + D, kind)
+    assert nat.solve_kernel(N, D, K, r, B=B) == "solve_dl_kernel"
+    kw = dict(free=True, n_free=True, cost=True, status=True)
+    dl = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    g = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, general=True, **kw)
+    np.testing.assert_array_equal(dl["status"], g["status"])
+    assert np.all(dl["status"] == 0)
+    np.testing.assert_array_equal(dl["n_free"], g["n_free"])
+    # (two FP64 orderings of the same solve: 1e-8, as the pattern pass against the column kernel)
+    assert scale_normalised_error(dl["coeffs"], g["coeffs"], times) <= 1e-8
+    nf = int(np.max(dl["n_free"]))
+    fscale = np.max(np.abs(g["free"][..., :nf]), axis=-1, keepdims=True) + 1.0
+    assert np.max(np.abs(dl["free"][..., :nf] - g["free"][..., :nf]) / fscale) <= 1e-8
+    assert np.max(np.abs(dl["cost"] - g["cost"]) / (np.abs(g["cost"]) + 1.0)) <= 1e-8
+    S = 64
+    ref = _oracle().solve_linear_batch(N, r, vals[:S], mask[:S].astype(np.uint32), times[:S])
+    if N <= 10:
+        assert scale_normalised_error(dl["coeffs"][:S], ref, times[:S]) <= 1e-6
+    else:  # the FP64 reference algorithm is itself ~1e-5 from truth at N = 12: 60-digit truth decides
+        import os
+        import sys
+        assert scale_normalised_error(dl["coeffs"][:S], ref, times[:S]) <= 1e-3
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+        from make_golden import truth_solve
+        for b in range(3):
+            tr = truth_solve(N, r, vals[b], mask[b], times[b])[0][None]
+            e_dl = scale_normalised_error(dl["coeffs"][b:b + 1], tr, times[b:b + 1])
+            e_or = scale_normalised_error(ref[b:b + 1], tr, times[b:b + 1])
+            assert e_dl <= max(1e-9, e_or), (b, e_dl, e_or)
+    assert check_path(vals, mask, times, dl["coeffs"], N, relative=True) < 1e-6
+
+
+def test_dl_general_masks_independent_of_batch_composition(gpu_ctx):
+    """Bits of a general-mask trajectory do not depend on its wave-mates: the whole mixed batch, reversed,
+    in chunks of 7, and singly."""
+    N, D, K, r = 10, 3, 10, 4
+    B = 300
+    vals, mask, times = _off_pattern_batch(N, D, K, B, 77, "mixed")
+    kw = dict(free=True, cost=True, status=True)
+    whole = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, **kw)
+    rev = gpu_ctx.solve_linear_batch(N, r, vals[::-1].copy(), mask[::-1].copy(), times[::-1].copy(), **kw)
+    for k in ("coeffs", "free", "cost", "status"):
+        np.testing.assert_array_equal(rev[k][::-1], whole[k], err_msg="reversed " + k)
+    for s0 in range(0, B, 7):
+        part = gpu_ctx.solve_linear_batch(N, r, vals[s0:s0 + 7], mask[s0:s0 + 7], times[s0:s0 + 7], **kw)
+        for k in ("coeffs", "free", "cost", "status"):
+            np.testing.assert_array_equal(part[k], whole[k][s0:s0 + 7], err_msg="chunk %d %s" % (s0, k))
+
+
+def test_dl_general_masks_dropped_orders_and_not_spd(gpu_ctx):
+    """General-mask pass status bits: mask bits above N/2-1 are dropped with WARN_DROPPED (lin_impl:74-95)
+    and the coefficients equal the solve without them; an overflowing segment time is NOT_SPD."""
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    N, D, K, r = 10, 3, 10, 4
+    B = 40
+    vals, mask, times = _off_pattern_batch(N, D, K, B, 5, "random")
+    hi = mask.copy()
+    hi[:, 3] |= np.uint8(0x60)
+    a = gpu_ctx.solve_linear_batch(N, r, vals, mask, times, status=True)
+    b = gpu_ctx.solve_linear_batch(N, r, vals, hi, times, status=True)
+    assert np.all(a["status"] == 0)
+    assert np.all(b["status"] & nat.MTG_TRAJ_WARN_DROPPED)
+    np.testing.assert_array_equal(a["coeffs"], b["coeffs"])
+    t2 = times.copy()
+    t2[3, 4] = 1e200
+    c = gpu_ctx.solve_linear_batch(N, r, vals, mask, t2, status=True)
+    assert c["status"][3] & nat.MTG_TRAJ_NOT_SPD
+    assert np.all(c["status"][np.arange(B) != 3] == 0)
