@@ -21,7 +21,10 @@ import mav_trajectory_generation_cmake_amd as mtg  # noqa: E402
 B = int(os.environ.get("B", "10000"))
 N, K, D = int(os.environ.get("N", "10")), int(os.environ.get("K", "10")), 3
 r = 4 if N == 10 else 3
-if N == 12:
+if os.environ.get("PATTERN") == "accel-ends":  # (the general-mask pass: ends fixed to ACCELERATION)
+    vals, mask, times = mtg.random_vertices_batch(N, D, K, B, [-50.0] * 3, [50.0] * 3, seed0=0, max_derivative=2,
+                                                  v_max=3.0, a_max=5.0)
+elif N == 12:
     vals, mask, times = mtg.random_vertices_batch(N, D, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=0,
                                                   max_derivative=4, v_max=3.0, a_max=5.0)
 else:
