@@ -227,13 +227,26 @@ int check_shape(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch) {
   return MTG_OK;
 }
 
+// MTG_HOST_WAIT=block: the pipeline's D2H thread sleeps on its chunk events (hipEventBlockingSync)
+// instead of spinning on them (the runtime's default).  For measuring the host work of several
+// concurrent pipelines (scripts/multi_host_cost.py): spinning waits make every waiting thread count
+// as a busy core.  Read once per process.
+bool host_wait_blocking() {
+  static const bool b = [] {
+    const char* v = getenv("MTG_HOST_WAIT");
+    return v && strcmp(v, "block") == 0;
+  }();
+  return b;
+}
+
 hipError_t ensure_pipe(mtg_ctx* ctx) {
   if (ctx->pipe_start) return hipSuccess;
+  const unsigned done_flags = hipEventDisableTiming | (host_wait_blocking() ? hipEventBlockingSync : 0u);
   for (auto& s : ctx->pipe) {
     hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.in_done, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.k_done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, done_flags);
     if (e != hipSuccess) return e;
   }
   hipError_t e = hipStreamCreateWithFlags(&ctx->pipe_h2d, hipStreamNonBlocking);
@@ -680,6 +693,9 @@ int mtg_create(int device, mtg_ctx** out_ctx) {
   if (!ctx) return MTG_ERR_OUT_OF_MEMORY;
   ctx->device = device;
   hipError_t e = hipSetDevice(device);
+  // (MTG_HOST_WAIT=block: every wait of the process's HIP runtime on this device sleeps, including
+  // the runtime's own waits inside pageable copies; measurement only, see host_wait_blocking)
+  if (e == hipSuccess && host_wait_blocking()) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = create_events(ctx, 1);
   if (e != hipSuccess) {
