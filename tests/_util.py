@@ -8,10 +8,12 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def golden_cases():
-    """The truth fixtures (tests/golden/make_golden.py); host_solve_bitwise.npz is a fixture of its own
-    (tests/golden/make_host_fixture.py, test_host_solver.py::test_host_solve_bitwise_fixture)."""
+    """The truth fixtures (tests/golden/make_golden.py); host_solve_bitwise.npz and
+    config4_truth_sample.npz are fixtures of their own (tests/golden/make_host_fixture.py,
+    tests/golden/make_config4_truth.py)."""
+    own = ("host_solve_bitwise.npz", "config4_truth_sample.npz")
     return sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not p.endswith("host_solve_bitwise.npz"))
+                  if os.path.basename(p) not in own)
 
 
 def load_golden(name):

@@ -219,3 +219,25 @@ def test_host_solve_bitwise_fixture():
             np.testing.assert_array_equal(out["free"][b, :, :nf[b]], g[key + "__free"][b, :, :nf[b]], err_msg=key)
         np.testing.assert_array_equal(out["cost"], g[key + "__cost"], err_msg=key)
         np.testing.assert_array_equal(out["status"], g[key + "__status"], err_msg=key)
+
+
+def test_host_solve_config4_truth_sample():
+    """The config-4 truth sample (tests/golden/make_config4_truth.py: 256 trajectories of the full-size
+    batch, 60-digit truth): the fixture's inputs still come out of the generator (SHA-256), and the host
+    solve of the sample is within 1e-9 of truth (5.8e-11 when the fixture was made) -- the CPU half of
+    the GPU test test_config4_full_size_truth_sample."""
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(here, "golden"))
+    import make_config4_truth as m
+    g = np.load(os.path.join(here, "golden", "config4_truth_sample.npz"))
+    vals, mask, times = m.batch()
+    idx = g["index"]
+    assert np.array_equal(idx, m.sample_index())
+    assert m.inputs_digest(vals, mask, times, idx) == str(g["inputs_sha256"])
+    h = mtg.host_solve_linear_batch(m.N, m.r, vals[idx], mask[idx], times[idx], status=True)
+    assert np.all(h["status"] == 0)
+    errs = [scale_normalised_error(h["coeffs"][i:i + 1], g["coeffs"][i:i + 1], times[idx][i:i + 1])
+            for i in range(len(idx))]
+    assert max(errs) <= 1e-9, max(errs)
