@@ -371,13 +371,36 @@ struct PairClock {
 // Trajectories per block (one wave) of the clock kernels: a lane pair each.
 constexpr int kPairTraj = 32;
 
+// The segment times of the wave's 32 trajectories, staged in LDS (LT) when they fit kClockLdsK per
+// trajectory.  Read from global memory inside the clock loop, each segment switch's load made the
+// compiler wait for vmcnt(0) at the next run -- which also waits for every run-table store the
+// wave has in flight, one store round trip per run.  LDS reads count on lgkmcnt only.
+constexpr int kClockLdsK = 256;
+
+template <bool LT>
+__device__ __forceinline__ const double* clock_times(const double* times, int K, int64_t B, int lane) {
+  const int64_t b0 = (int64_t)blockIdx.x * kPairTraj;
+  const int64_t b = b0 + (lane >> 1);
+  if constexpr (LT) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int nv = (int)(B - b0 < kPairTraj ? B - b0 : kPairTraj);
+    const double* src = times + b0 * K;
+    for (int j = lane; j < nv * K; j += 64) lds[j] = src[j];
+    __syncthreads();  // (one wave)
+    return lds + (b < B ? (int)(b - b0) : 0) * K;
+  } else {
+    return times + (b < B ? b : 0) * K;
+  }
+}
+
+template <bool LT>
 __global__ __launch_bounds__(64) void eval_count_kernel(int K, int64_t B, const double* times, double t_start,
                                                         double t_end, double dt, int64_t* counts) {
   const int lane = threadIdx.x;
   const int64_t b = (int64_t)blockIdx.x * kPairTraj + (lane >> 1);
   const bool valid = b < B;
   PairClock ck;
-  ck.init(times + (valid ? b : 0) * K, K, t_start, t_end, dt, lane & 1, valid);
+  ck.init(clock_times<LT>(times, K, B, lane), K, t_start, t_end, dt, lane & 1, valid);
   while (ck.next(nullptr)) {
   }
   if (valid && !(lane & 1)) counts[b] = ck.n;
@@ -394,6 +417,7 @@ __global__ __launch_bounds__(64) void eval_count_kernel(int K, int64_t B, const 
 // clock twice -- and, per 32-trajectory block (one wave), writes the exclusive prefix sum of the
 // counts inside the block to offs[b] and the block's total to bsum[block]: the first level of the
 // device-side offsets (eval_scan_kernel, then the eval kernel adds the block's offset).
+template <bool LT>
 __global__ __launch_bounds__(64) void eval_runs_kernel(int K, int64_t B, const double* times, double t_start,
                                                        double t_end, double dt, int cap, RunHead* heads, RunRec* runs,
                                                        int64_t* counts, int64_t* offs, int64_t* bsum) {
@@ -402,7 +426,7 @@ __global__ __launch_bounds__(64) void eval_runs_kernel(int K, int64_t B, const d
   const int64_t b = (int64_t)blockIdx.x * kPairTraj + (lane >> 1);
   const bool valid = b < B;
   PairClock ck;
-  ck.init(times + (valid ? b : 0) * K, K, t_start, t_end, dt, odd, valid);
+  ck.init(clock_times<LT>(times, K, B, lane), K, t_start, t_end, dt, odd, valid);
   RunRec* rr = runs + (valid ? b : 0) * (int64_t)cap;
   int64_t nr = 0;
   while (nr < cap && ck.next(rr + nr)) ++nr;
@@ -813,8 +837,12 @@ hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times
   // 2 on 40 CUs: 0.163 -> 0.154 ms, round 2)
   const int64_t grid = (B + kPairTraj - 1) / kPairTraj;
   if (grid == 0) return hipSuccess;
-  launch_kernel(eval_count_kernel, dim3((unsigned)grid), dim3(64), 0, stream, K, B, times, t_start, t_end, dt,
-                counts);
+  if (K <= kClockLdsK)
+    launch_kernel(eval_count_kernel<true>, dim3((unsigned)grid), dim3(64), (uint32_t)(sizeof(double) * kPairTraj * K),
+                  stream, K, B, times, t_start, t_end, dt, counts);
+  else
+    launch_kernel(eval_count_kernel<false>, dim3((unsigned)grid), dim3(64), 0, stream, K, B, times, t_start, t_end, dt,
+                  counts);
   return hipGetLastError();
 }
 
@@ -843,8 +871,12 @@ hipError_t launch_eval_runs_counts(int K, int64_t B, const double* times, double
   RunRec* runs = reinterpret_cast<RunRec*>(heads + B);
   int64_t* bsum = reinterpret_cast<int64_t*>(runs + (size_t)B * cap);
   const int64_t nb = (B + kPairTraj - 1) / kPairTraj;
-  launch_kernel(eval_runs_kernel, dim3((unsigned)nb), dim3(64), 0, stream, K, B, times, t_start, t_end, dt, cap,
-                heads, runs, counts, offsets, bsum);
+  if (K <= kClockLdsK)
+    launch_kernel(eval_runs_kernel<true>, dim3((unsigned)nb), dim3(64), (uint32_t)(sizeof(double) * kPairTraj * K),
+                  stream, K, B, times, t_start, t_end, dt, cap, heads, runs, counts, offsets, bsum);
+  else
+    launch_kernel(eval_runs_kernel<false>, dim3((unsigned)nb), dim3(64), 0, stream, K, B, times, t_start, t_end, dt,
+                  cap, heads, runs, counts, offsets, bsum);
   hipLaunchKernelGGL(eval_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, nb, bsum, total);
   return hipGetLastError();
 }
@@ -864,8 +896,14 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
     if (runs_ready) {  // launch_eval_runs_counts filled the table, the in-block offsets and the block offsets
       boff = reinterpret_cast<const int64_t*>(runs + (size_t)B * cap);
     } else {
-      launch_kernel(eval_runs_kernel, dim3((unsigned)((B + kPairTraj - 1) / kPairTraj)), dim3(64), 0, stream, K, B, times,
-                    t_start, t_end, dt, cap, heads, runs, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
+      const dim3 g((unsigned)((B + kPairTraj - 1) / kPairTraj));
+      if (K <= kClockLdsK)
+        launch_kernel(eval_runs_kernel<true>, g, dim3(64), (uint32_t)(sizeof(double) * kPairTraj * K), stream, K, B,
+                      times, t_start, t_end, dt, cap, heads, runs, (int64_t*)nullptr, (int64_t*)nullptr,
+                      (int64_t*)nullptr);
+      else
+        launch_kernel(eval_runs_kernel<false>, g, dim3(64), 0, stream, K, B, times, t_start, t_end, dt, cap, heads,
+                      runs, (int64_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr);
     }
   }
   // D = 3 (every reference problem in 3-D) has its own kernels: the sample loop's dimensions unrolled
