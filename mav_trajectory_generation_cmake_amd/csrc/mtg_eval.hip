@@ -829,6 +829,236 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
   }
 }
 
+// The stored-run sample loop for D = 3 as a producer / consumer pair (MTG_EVAL_PC): a block of two
+// waves per trajectory, wave 0 evaluating the samples block by block into one of two LDS slots,
+// wave 1 storing the other slot's rows and sample times.  In the one-wave kernel the same wave
+// computed and stored, and a store that could not issue (the memory queue full) held up its
+// compute; the kernel took ~0.63 ms where its compute alone took ~0.39 and its stores alone ~0.44.
+// The two waves meet at one s_barrier per block; the barrier waits only for LDS (the store wave's
+// global stores stay in flight).  Samples, rows and their order are the one-wave kernel's exactly.
+#ifndef MTG_EVAL_PC
+#define MTG_EVAL_PC 1
+#endif
+#ifndef MTG_EVAL_PC_WAVES
+#define MTG_EVAL_PC_WAVES 5
+#endif
+struct PcSlot {
+  double v[kSpl * kEvalThreads * 3];  // the block's rows, sample-major
+  double ts[kSpl * kEvalThreads];     // its sample times
+  int64_t nb;                         // its first sample (trajectory-relative)
+  int cnt;                            // its samples; 0: the trajectory is done
+  int pad;
+};
+static_assert(sizeof(PcSlot) % 16 == 0, "slots stay 16-B aligned");
+
+// s_barrier after this wave's LDS accesses; unlike __syncthreads, no wait for its global stores
+__device__ __forceinline__ void pc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int N, int DER>
+__global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_eu(MTG_EVAL_PC_WAVES))) void eval_range_pc_kernel(
+    int K, const double* coeffs, int derivative, const int64_t* counts, const int64_t* offsets, double* out,
+    double* sample_times, int cap, const RunHead* heads, const RunRec* runs, const int64_t* boff,
+    int64_t* offsets_out, int64_t capacity, const int64_t* total) {
+#pragma clang fp contract(off)
+  constexpr int DD = 3;
+  constexpr int kBlk = kSpl * kEvalThreads;
+  constexpr int P16 = kBlk * DD / (2 * kEvalThreads);
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t n_total = counts[b];
+  const RunHead h = heads[b];
+  if (!stored_whole(h, n_total, DD)) return;  // (the rest launch takes it)
+  const int64_t base = boff ? offsets[b] + boff[b / kPairTraj] : offsets[b];
+  if (boff && tid == 0) offsets_out[b] = base;
+  if (n_total <= 0 || base + n_total > capacity || (total && *total > capacity)) return;
+  RunLds* rt = reinterpret_cast<RunLds*>(lds);
+  double* cf = reinterpret_cast<double*>(rt + 1);       // [K][3][N]
+  PcSlot* slot = reinterpret_cast<PcSlot*>(cf + K * DD * N);  // [2]
+  if (DER >= 0) derivative = DER;
+  const double* cb = coeffs + b * (int64_t)K * DD * N;
+  for (int i = tid; i < K * DD * N; i += 2 * kEvalThreads) cf[i] = base_coeff(derivative, i % N) * cb[i];
+  __syncthreads();
+
+  if (wave == 1) {  // ---- the store wave
+    const bool al16 = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out + base * DD, (uint32_t)(n_total * DD * 8));
+    const __amdgpu_buffer_rsrc_t rs =
+        buf_rsrc(sample_times ? sample_times + base : out, sample_times ? (uint32_t)(n_total * 8) : 0u);
+    for (int i = 0;; ++i) {
+      pc_barrier();
+      const PcSlot* sl = slot + (i & 1);
+      const int cnt = sl->cnt;
+      if (cnt == 0) break;
+      const int64_t nb = sl->nb;
+      double tv[kSpl];
+#pragma unroll
+      for (int q = 0; q < kSpl; ++q) tv[q] = sl->ts[q * kEvalThreads + lane];
+#if MTG_EVAL_EXP == 3
+      const uint32_t o0 = kBufOOB;  // (diagnostic builds: every store dropped)
+#else
+      const uint32_t o0 = (uint32_t)(nb * DD * 8);
+#endif
+      if (cnt == kBlk && al16) {
+        dvec2 w[P16];
+#pragma unroll
+        for (int u = 0; u < P16; ++u) w[u] = reinterpret_cast<const dvec2*>(sl->v)[u * kEvalThreads + lane];
+        lds_fence();  // (read before the barrier lets the compute wave refill the slot)
+#pragma unroll
+        for (int u = 0; u < P16; ++u)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, w[u]), ro, o0 + (uint32_t)(u * kEvalThreads + lane) * 16, 0, 0);
+      } else {
+        double w[kSpl * DD];
+#pragma unroll
+        for (int u = 0; u < kSpl * DD; ++u) w[u] = sl->v[u * kEvalThreads + lane];
+        lds_fence();
+#pragma unroll
+        for (int u = 0; u < kSpl * DD; ++u)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, w[u]), ro,
+                                                u * kEvalThreads + lane < cnt * DD ? o0 + (uint32_t)(u * kEvalThreads + lane) * 8 : kBufOOB, 0, 0);
+      }
+      if (sample_times) {
+#pragma unroll
+        for (int q = 0; q < kSpl; ++q)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, tv[q]), rs,
+                                                q * kEvalThreads + lane < cnt && MTG_EVAL_EXP != 3 ? (uint32_t)((nb + q * kEvalThreads + lane) * 8) : kBufOOB, 0, 0);
+      }
+    }
+    return;
+  }
+
+  // ---- the compute wave: the runs from the table, 32 per round; blocks of kBlk samples
+  const RunRec* rr = runs + b * (int64_t)cap;
+  const int64_t stored = h.nruns, stored_end = h.n;
+  int64_t next_run = 0;
+  int blk = 0;
+  double cc[DD * N];  // the cached segment's Horner terms (wave-uniform: SGPRs)
+  int cseg = -1;
+  while (next_run < stored) {
+    const int nr = (int)(stored - next_run < kRuns ? stored - next_run : kRuns);
+    if (lane < nr) {
+      const RunRec w = rr[next_run + lane];
+      rt->n0[lane] = w.n0;
+      rt->tm[lane] = w.tm;
+      rt->ti[lane] = w.ti;
+      rt->tE[lane] = w.tE;
+      rt->am[lane] = w.am;
+      rt->ai[lane] = w.ai;
+      rt->aE[lane] = w.aE;
+      rt->tin0[lane] = w.tin0;
+      rt->acc0[lane] = w.acc0;
+      rt->seg[lane] = w.segs >> 1;
+      rt->single[lane] = w.segs & 1;
+    }
+    const int64_t round_end = next_run + nr < stored ? rr[next_run + nr].n0 : stored_end;
+    next_run += nr;
+    lds_fence();
+    const int64_t first = rt->n0[0], end = round_end < n_total ? round_end : n_total;
+    int ri = 0;
+    int64_t nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;
+    for (int64_t nb = first; nb < end;) {
+      int cnt = (int)(end - nb < kBlk ? end - nb : kBlk);
+      if ((((base + nb) & 1) != 0) && cnt == kBlk) cnt = kBlk - 1;  // (rows 16-B aligned from the next block on)
+      PcSlot* sl = slot + (blk & 1);
+      double tv[kSpl];
+      int sg[kSpl];
+#pragma unroll
+      for (int q = 0; q < kSpl; ++q) {
+        const int64_t n = nb + q * kEvalThreads + lane;
+        const bool have = q * kEvalThreads + lane < cnt;
+        while (have && nxt <= n) {
+          ++ri;
+          nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;
+        }
+        const int64_t k = n - rt->n0[ri];
+        double t, a;
+        if (rt->single[ri]) {
+          t = rt->tin0[ri];
+          a = rt->acc0[ri];
+        } else {
+          t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
+          a = sample_times ? mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]) : 0.0;
+        }
+        tv[q] = t;
+        sg[q] = rt->seg[ri];
+        sl->ts[q * kEvalThreads + lane] = a;
+      }
+      double v[kSpl][DD];
+      const int sg0 = __builtin_amdgcn_readfirstlane(sg[0]);
+      bool same = true;
+#pragma unroll
+      for (int q = 0; q < kSpl; ++q) same = same && sg[q] == sg0;
+      if (__builtin_amdgcn_ballot_w64(!same) == 0) {
+        if (sg0 != cseg) {
+          const double* c0 = cf + (sg0 * DD) * N;
+#pragma unroll
+          for (int i = 0; i < DD * N; ++i) {
+            const uint64_t w = __builtin_bit_cast(uint64_t, c0[i]);
+            const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+            const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)w);
+            cc[i] = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+          }
+          cseg = sg0;
+        }
+#pragma unroll
+        for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+          for (int d = 0; d < DD; ++d) v[q][d] = derivative < N ? cc[d * N + N - 1] : 0.0;
+        if (derivative < N) {
+#pragma unroll
+          for (int j = N - 2; j >= 0; --j) {
+            if (DER >= 0 ? j >= DER : j >= derivative) {
+#pragma unroll
+              for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+                for (int d = 0; d < DD; ++d) {
+                  v[q][d] = v[q][d] * tv[q];
+                  v[q][d] = v[q][d] + cc[d * N + j];
+                }
+            }
+          }
+        }
+      } else {
+        const double* cs[kSpl];
+#pragma unroll
+        for (int q = 0; q < kSpl; ++q) cs[q] = cf + (sg[q] * DD) * N;
+#pragma unroll
+        for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+          for (int d = 0; d < DD; ++d) v[q][d] = derivative < N ? cs[q][d * N + N - 1] : 0.0;
+        if (derivative < N) {
+#pragma unroll
+          for (int j = N - 2; j >= 0; --j) {
+            if (DER >= 0 ? j >= DER : j >= derivative) {
+#pragma unroll
+              for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+                for (int d = 0; d < DD; ++d) {
+                  v[q][d] = v[q][d] * tv[q];
+                  v[q][d] = v[q][d] + cs[q][d * N + j];
+                }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+        for (int d = 0; d < DD; ++d) sl->v[(q * kEvalThreads + lane) * DD + d] = v[q][d];
+      if (lane == 0) {
+        sl->nb = nb;
+        sl->cnt = cnt;
+      }
+      pc_barrier();  // the slot to the store wave
+      ++blk;
+      nb += cnt;
+    }
+    if (end >= n_total) break;
+  }
+  if (lane == 0) slot[blk & 1].cnt = 0;  // done
+  pc_barrier();
+}
+
 hipError_t launch_eval_count(int N, int D, int K, int64_t B, const double* times, double t_start,
                              double t_end, double dt, int64_t* counts, hipStream_t stream) {
   (void)N;
@@ -913,6 +1143,8 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   // block reloads the run table and stages the coefficients.)
   const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)(d3 ? kSpl : 1) * kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
+  const size_t lds_pc = sizeof(RunLds) + sizeof(double) * (size_t)K * 3 * N + 2 * sizeof(PcSlot);
+  const bool pc = MTG_EVAL_PC && lds_pc <= 64 * 1024;  // (else the one-wave kernel)
   const dim3 grid((unsigned)B);
   // D = 3 with the run table: an ST launch takes every trajectory whose whole clock is in it, and
   // the run-time-D kernel (rest) the others -- its blocks for the stored ones return at once
@@ -922,7 +1154,14 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   const bool stored = MTG_EVAL_STORED && heads != nullptr && d3;
 #define MTG_EVAL_LAUNCH(NN, DER)                                                                                   \
   do {                                                                                                             \
-    if (stored) {                                                                                                  \
+    if (stored && pc) {                                                                                            \
+      launch_kernel(eval_range_pc_kernel<NN, DER>, grid, dim3(2 * kEvalThreads), lds_pc, stream, K, coeffs,        \
+                    derivative, counts, offsets, out, sample_times, cap, heads, runs, boff, offsets_out, capacity, \
+                    total);                                                                                        \
+      launch_kernel(eval_range_kernel<NN, DER, 0, false>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,     \
+                    times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
+                    boff, offsets_out, capacity, total, true);                                                     \
+    } else if (stored) {                                                                                           \
       launch_kernel(eval_range_kernel<NN, DER, 3, true>, grid, dim3(kEvalThreads), lds, stream, D, K, coeffs,      \
                     times, t_start, t_end, dt, derivative, counts, offsets, out, sample_times, cap, heads, runs,  \
                     boff, offsets_out, capacity, total, false);                                                    \

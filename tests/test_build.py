@@ -32,10 +32,15 @@ def _kernel_bodies(asm, prefix):
 def test_evaluate_range_has_no_fma(tmp_path):
     """Polynomial::evaluate (polynomial.h:138-151) multiplies then adds; an FMA would change the
     last bit and break bit-exact parity of evaluateRange with the reference."""
-    bodies = _kernel_bodies(_device_asm("mtg_eval.hip", tmp_path), r"_ZN3mtg17eval_range_kernel")
+    asm = _device_asm("mtg_eval.hip", tmp_path)
+    bodies = _kernel_bodies(asm, r"_ZN3mtg17eval_range_kernel")
     # N = 2, 4, ..., 12 x derivative 0..4 and the runtime-derivative variant x (D = 3, D = 3 stored-run
     # only (ST), run-time D)
     assert len(bodies) == 108
+    # the producer / consumer form of the stored-run D = 3 kernel: N x derivative
+    pc = _kernel_bodies(asm, r"_ZN3mtg20eval_range_pc_kernel")
+    assert len(pc) == 36
+    bodies.update(pc)
     for name, body in bodies.items():
         # f64 FMAs are allowed only as the compiler's f64 -> int64 conversion idiom (x - 2^32 hi,
         # constant 0xc1f00000) in the clock's integer run arithmetic; f32 FMAs belong to its
