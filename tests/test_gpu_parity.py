@@ -920,6 +920,41 @@ def test_min_max_magnitude_edge_shapes(gpu_ctx, N, K, D, B, derivative):
             assert np.all((a["segment"] >= 0) & (a["segment"] < K))
 
 
+def test_evaluate_range_sample_kernel_store_paths(gpu_ctx):
+    """The producer / consumer sample kernel's store paths (round 5): rows to an output that is only
+    8-B aligned (8-B row pieces instead of 16-B), and no sample-time output, give the same rows as the
+    16-B-aligned call with times; 3 trajectories of the misaligned call against the oracle, bit-exact."""
+    torch = pytest.importorskip("torch")
+    from mav_trajectory_generation_cmake_amd import _native as nat
+    from mav_trajectory_generation_cmake_amd.solver import _addr
+    O = _oracle()
+    B = 300
+    vals, mask, times = _bench_batch(B, seed0=37, K=10)
+    coeffs = gpu_ctx.solve_linear_batch(10, 4, vals, mask, times)["coeffs"]
+    ref_out, ref_st, counts, offs = gpu_ctx.evaluate_range_batch(coeffs, times, 0.0, 1e9, 0.01, 0)
+    no_t = gpu_ctx.evaluate_range_batch(coeffs, times, 0.0, 1e9, 0.01, 0, want_times=False)
+    assert no_t[1] is None
+    np.testing.assert_array_equal(no_t[0], ref_out)
+    total = int(counts.sum())
+    c_d, t_d = torch.from_numpy(coeffs).cuda(), torch.from_numpy(times).cuda()
+    cnt_d, off_d = torch.from_numpy(counts).cuda(), torch.from_numpy(offs).cuda()
+    buf = torch.full((total * 3 + 1,), 7.25, dtype=torch.float64, device="cuda")
+    out_view = buf[1:]  # 8-B aligned only
+    assert out_view.data_ptr() % 16 == 8
+    gpu_ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    nat.check(gpu_ctx._lib.mtg_evaluate_range_batch(gpu_ctx.handle, 10, 3, 10, B, _addr(c_d), _addr(t_d), 0.0, 1e9,
+                                                    0.01, 0, _addr(cnt_d), _addr(off_d), _addr(out_view), None,
+                                                    nat.MTG_FLAG_DEVICE_PTRS), gpu_ctx.handle)
+    torch.cuda.synchronize()
+    got = out_view.cpu().numpy().reshape(total, 3)
+    assert buf[0].item() == 7.25
+    np.testing.assert_array_equal(got, ref_out)
+    for b in (0, 151, 299):
+        ro, rst, n = O.evaluate_range(coeffs[b], times[b], 0.0, 1e9, 0.01, 0, max_samples=int(counts[b]) + 10)
+        assert n == counts[b]
+        np.testing.assert_array_equal(got[offs[b]:offs[b] + n], ro)
+
+
 @pytest.mark.parametrize("B", [1, 130, 2000])
 def test_evaluate_range_full_one_call(gpu_ctx, B):
     """mtg_evaluate_range_batch_full: counts, offsets (device-side two-level scan) and samples in one
