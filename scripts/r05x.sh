@@ -3,5 +3,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r05x
-bash scripts/eval_ab.sh default pcf3 pcf4 > gpurun_out/r05x/eval_ab.log 2>&1; rc=$?; cat gpurun_out/r05x/eval_ab.log; exit $rc
+mkdir -p gpurun_out/${EVO:-r05x}
+bash scripts/eval_ab.sh ${EVV:-default pcf3 pcf4} > gpurun_out/${EVO:-r05x}/eval_ab.log 2>&1; rc=$?; cat gpurun_out/${EVO:-r05x}/eval_ab.log; exit $rc
