@@ -542,7 +542,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
   if constexpr (ST) {
     if (!stored_whole(heads[b], n_total, D)) return;
   } else {
-    if (rest && stored_whole(heads[b], n_total, D)) return;  // (the ST launch has taken it)
+    if (rest && stored_whole(heads[b], n_total, D)) return;  // (the stored-run launch has taken it)
   }
   // offsets: given (offsets[b]), or device-side (the in-block prefix offsets[b] + the block's offset)
   const int64_t base = boff ? offsets[b] + boff[b / kPairTraj] : offsets[b];
@@ -1146,8 +1146,9 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   const size_t lds_pc = sizeof(RunLds) + sizeof(double) * (size_t)K * 3 * N + 2 * sizeof(PcSlot);
   const bool pc = MTG_EVAL_PC && lds_pc <= 64 * 1024;  // (else the one-wave kernel)
   const dim3 grid((unsigned)B);
-  // D = 3 with the run table: an ST launch takes every trajectory whose whole clock is in it, and
-  // the run-time-D kernel (rest) the others -- its blocks for the stored ones return at once
+  // D = 3 with the run table: a stored-run launch takes every trajectory whose whole clock is in it
+  // (the producer / consumer kernel, or the one-wave ST kernel when its LDS would not fit), and the
+  // run-time-D kernel (rest) the others -- its blocks for the stored ones return at once
 #ifndef MTG_EVAL_STORED
 #define MTG_EVAL_STORED 1  // (0: one launch of the D = 3 kernel with the lane-0 clock, for A/B builds)
 #endif
