@@ -988,6 +988,14 @@ __global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_e
       bool same = true;
 #pragma unroll
       for (int q = 0; q < kSpl; ++q) same = same && sg[q] == sg0;
+#if MTG_EVAL_EXP == 2
+      if (true) {  // (diagnostic builds: no Horner)
+#pragma unroll
+        for (int q = 0; q < kSpl; ++q)
+#pragma unroll
+          for (int d = 0; d < DD; ++d) v[q][d] = tv[q] + d;
+      } else
+#endif
       if (__builtin_amdgcn_ballot_w64(!same) == 0) {
         if (sg0 != cseg) {
           const double* c0 = cf + (sg0 * DD) * N;

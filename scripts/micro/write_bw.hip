@@ -7,6 +7,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -o scripts/micro/write_bw scripts/micro/write_bw.hip
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 
 constexpr size_t kBytes = size_t(2380) << 20;
@@ -78,6 +79,38 @@ __global__ __launch_bounds__(64) void pat2(double* __restrict__ rows, double* __
   }
 }
 
+// the same with evaluateRange's spread of samples per trajectory (3300..11596, mean 7448, like the
+// 1e4 config-2 batch's 3289..12229): trajectory b = order[block] has cnt[b] samples at offset off[b]
+template <int FLOPS>
+__global__ __launch_bounds__(64) void pat2v(double* __restrict__ rows, double* __restrict__ st, const int* __restrict__ cnt,
+                                            const long long* __restrict__ off, const int* __restrict__ order, double x0) {
+  const int l = threadIdx.x;
+  const int b = order[blockIdx.x];
+  const int n = cnt[b];
+  const long long o = off[b] & ~1ll;  // (rows 16-B aligned)
+  double2* rp = reinterpret_cast<double2*>(rows + o * 3);
+  double* sp = st + o;
+  for (int nb = 0; nb + 128 <= n; nb += 128) {
+    double v[6];
+    const double t0 = x0 + nb + l, t1 = t0 + 64.0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v[c] = (c < 3 ? t0 : t1) * 0.5;
+    if (FLOPS) {
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          v[c] = v[c] * (c < 3 ? t0 : t1);
+          v[c] = v[c] + 0.25;
+        }
+    }
+    sp[nb + l] = t0;
+    sp[nb + 64 + l] = t1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) rp[nb * 3 / 2 + u * 64 + l] = make_double2(v[2 * u], v[2 * u + 1]);
+  }
+}
+
 template <class F>
 static float timeit(F f) {
   hipEvent_t e0, e1;
@@ -116,6 +149,38 @@ int main() {
       double* st = a + (size_t)kTraj * kSamples * 3;
       rep2("pat2", timeit([&] { hipLaunchKernelGGL(pat2<0>, dim3(kTraj), dim3(64), 0, 0, a, st, 1.0); }));
       rep2("pat2_flop", timeit([&] { hipLaunchKernelGGL(pat2<1>, dim3(kTraj), dim3(64), 0, 0, a, st, 1.0); }));
+    }
+  }
+  {
+    // variable samples per trajectory: index order, and longest first
+    int h_cnt[kTraj], h_ord[kTraj], h_srt[kTraj];
+    long long h_off[kTraj], acc = 0;
+    for (int b = 0; b < kTraj; ++b) {
+      h_cnt[b] = 3300 + (int)(((unsigned)b * 2654435761u >> 8) % 8296u);
+      h_off[b] = acc;
+      acc += h_cnt[b];
+      h_ord[b] = b;
+      h_srt[b] = b;
+    }
+    std::sort(h_srt, h_srt + kTraj, [&](int x, int y) { return h_cnt[x] > h_cnt[y]; });
+    const size_t rows = (size_t)acc * 3 * 8, sts = (size_t)acc * 8;
+    if (rows + sts + 64 <= kBytes) {
+      int *d_cnt, *d_ord, *d_srt;
+      long long* d_off;
+      hipMalloc(&d_cnt, sizeof(h_cnt));
+      hipMalloc(&d_ord, sizeof(h_ord));
+      hipMalloc(&d_srt, sizeof(h_srt));
+      hipMalloc(&d_off, sizeof(h_off));
+      hipMemcpy(d_cnt, h_cnt, sizeof(h_cnt), hipMemcpyHostToDevice);
+      hipMemcpy(d_ord, h_ord, sizeof(h_ord), hipMemcpyHostToDevice);
+      hipMemcpy(d_srt, h_srt, sizeof(h_srt), hipMemcpyHostToDevice);
+      hipMemcpy(d_off, h_off, sizeof(h_off), hipMemcpyHostToDevice);
+      double* st = a + (size_t)acc * 3 + 2;
+      auto rep3 = [&](const char* name, float ms) {
+        std::printf("%-10s %8.1f us  %6.2f TB/s\n", name, ms * 1e3, (rows + sts) / (ms * 1e-3) / 1e12);
+      };
+      rep3("pat2v", timeit([&] { hipLaunchKernelGGL(pat2v<1>, dim3(kTraj), dim3(64), 0, 0, a, st, d_cnt, d_off, d_ord, 1.0); }));
+      rep3("pat2v_lpt", timeit([&] { hipLaunchKernelGGL(pat2v<1>, dim3(kTraj), dim3(64), 0, 0, a, st, d_cnt, d_off, d_srt, 1.0); }));
     }
   }
   rep("memset", timeit([&] { hipMemsetAsync(a, 0, tot); }));
