@@ -73,19 +73,44 @@ def max_over_ranks(x, dist):
     return float(t.item())
 
 
-def traffic_from_profiles(kernel_prefix, batch, workload):
-    """HBM bytes per launch of the kernel from the committed PMC summary (profiles/), or None.  Keyed
-    by kernel and workload (scripts/summarize_profiles.py)."""
+def csrc_digest():
+    """SHA-256 over the kernel sources (mav_trajectory_generation_cmake_amd/csrc, names and contents):
+    the build identity a PMC capture is valid for."""
+    import hashlib
+    d = os.path.join(ROOT, "mav_trajectory_generation_cmake_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".inc", ".h", ".cpp", ".py")):
+            h.update(f.encode())
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()
+
+
+def traffic_key(kernel_prefix, workload, pattern="generator"):
+    """profiles/pmc_traffic.json key of a capture: kernel, bench workload and vertex pattern."""
+    return "%s|%s|%s" % (kernel_prefix, workload, pattern)
+
+
+def traffic_from_profiles(kernel_prefix, batch, workload, pattern="generator"):
+    """HBM bytes per launch of the kernel from the committed PMC summary (profiles/), and where they
+    come from: (bytes, source) or (None, reason).  A capture is used only for the same kernel, workload,
+    vertex pattern and batch, taken on a build of the same kernel sources (csrc_digest) -- otherwise
+    the line carries traffic null (scripts/summarize_profiles.py writes the captures)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, "no profiles/pmc_traffic.json"
     try:
         with open(path) as f:
             d = json.load(f)
-        ent = d.get("%s|%s" % (kernel_prefix, workload), {}).get(str(batch))
-        return None if ent is None else float(ent["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+        ent = d.get(traffic_key(kernel_prefix, workload, pattern), {}).get(str(batch))
+        if ent is None:
+            return None, "no PMC capture of %s for this workload / pattern / batch" % kernel_prefix
+        if ent.get("csrc_sha256") != csrc_digest():
+            return None, "the PMC capture (%s) is of other kernel sources" % ent.get("profile")
+        return float(ent["hbm_bytes_per_launch"]), ent.get("profile")
+    except Exception as e:  # (a malformed summary is not a measurement)
+        return None, "unreadable pmc_traffic.json: %s" % e
 
 
 def _oracle_lib():
@@ -460,7 +485,7 @@ def main():
     total = units * world * args.steps
     value = total / el
     achieved = bpt * B / (kern_ms * 1e-3) / 1e9
-    traffic = traffic_from_profiles(kname, B, wl)
+    traffic, traffic_src = traffic_from_profiles(kname, B, wl, args.pattern)
     out = {
         "metric": metric,
         "value": value,
@@ -480,6 +505,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": kname,
                      "kernel_ms": kern_ms,
                      "kernel_ms_method": "HIP events around the timed region on the launch stream / steps "

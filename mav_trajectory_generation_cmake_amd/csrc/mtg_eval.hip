@@ -236,7 +236,8 @@ struct Clock {
 
 // A run as stored in the HBM run table (eval_runs_kernel -> eval_range_kernel), 64 B.  Its length is
 // the next run's n0 less its own (the last stored run ends at RunHead::n); segs = 2 seg + single.
-// The tin lane of eval_runs_kernel's lane pair writes bytes 0-31 and 56-63, the acc lane 32-55.
+// The tin lane of eval_runs_kernel's lane pair writes bytes 0-31 and 56-61 (n0, tm, ti, tin0, segs,
+// tE), the acc lane 32-55 and 62-63 (am, ai, acc0, aE).
 struct RunRec {
   int64_t n0, tm, ti;
   double tin0;
@@ -459,7 +460,8 @@ __global__ __launch_bounds__(64) void eval_runs_kernel(int K, int64_t B, const d
 }
 
 // Second level of the offsets: one block scans the per-block totals in place (exclusive) and writes
-// the grand total.  nb = ceil(B / 64) entries; each thread takes a contiguous chunk.
+// the grand total.  nb = ceil(B / kPairTraj) entries (one per 32-trajectory block of the clock
+// kernel); each thread takes a contiguous chunk.
 constexpr int kScanThreads = 1024;
 __global__ __launch_bounds__(kScanThreads) void eval_scan_kernel(int64_t nb, int64_t* bsum, int64_t* total) {
   __shared__ int64_t part[kScanThreads];

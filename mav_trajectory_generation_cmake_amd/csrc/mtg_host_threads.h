@@ -38,14 +38,28 @@ inline int cgroup_dir_cpus(const std::string& dir, bool v2) {
   return quota / period > 0 ? (int)(quota / period) : 1;
 }
 
-// The tightest quota over the process's cgroup and its ancestors.  root: where the hierarchy is
-// mounted (/sys/fs/cgroup, or its cpu controller's directory for v1); proc_cgroup: the contents of
-// /proc/self/cgroup ("0::/path" for v2, "N:cpu,cpuacct:/path" for v1).  Without a cgroup
+// The tightest quota over the process's cgroup and its ancestors.  root_v2: where the unified
+// hierarchy is mounted (/sys/fs/cgroup); root_v1: the v1 cpu controller's directory; proc_cgroup: the
+// contents of /proc/self/cgroup ("0::/path" for v2, "N:cpu,cpuacct:/path" for v1).  A hybrid host
+// (systemd's hybrid mode) has both lines: the v2 walk finds no cpu.max there (the controller is in
+// the v1 tree), so both hierarchies are walked and the smaller quota is taken.  Without a cgroup
 // namespace the path is the full one and the walk visits every ancestor; inside one (the path is
 // "/") it reads the namespace root, which is the container's own quota.  0: no quota found.
+inline int cgroup_walk_cpus(const std::string& root, std::string path, bool v2) {
+  int best = 0;
+  for (;;) {  // this cgroup, then each ancestor up to the mount root
+    const int c = cgroup_dir_cpus(root + (path == "/" ? "" : path), v2);
+    if (c > 0 && (best == 0 || c < best)) best = c;
+    if (path.empty() || path == "/") break;
+    const size_t s = path.find_last_of('/');
+    path = s == 0 || s == std::string::npos ? "/" : path.substr(0, s);
+  }
+  return best;
+}
+
 inline int cgroup_quota_cpus(const std::string& root_v2, const std::string& root_v1, const std::string& proc_cgroup) {
-  std::string path;
-  bool v2 = false, found = false;
+  std::string p2, p1;
+  bool has2 = false, has1 = false;
   size_t pos = 0;
   while (pos < proc_cgroup.size()) {
     size_t end = proc_cgroup.find('\n', pos);
@@ -56,32 +70,25 @@ inline int cgroup_quota_cpus(const std::string& root_v2, const std::string& root
     if (c2 == std::string::npos) continue;
     const std::string ctrl = line.substr(c1 + 1, c2 - c1 - 1);
     if (line.compare(0, c1, "0") == 0 && ctrl.empty()) {  // v2 unified hierarchy
-      path = line.substr(c2 + 1);
-      v2 = found = true;
-    } else if (!found || !v2) {  // v1: the line naming the cpu controller
+      p2 = line.substr(c2 + 1);
+      has2 = true;
+    } else {  // v1: the line naming the cpu controller
       size_t p = 0;
       while (p <= ctrl.size()) {
         size_t q = ctrl.find(',', p);
         if (q == std::string::npos) q = ctrl.size();
         if (ctrl.compare(p, q - p, "cpu") == 0) {
-          path = line.substr(c2 + 1);
-          found = true;
+          p1 = line.substr(c2 + 1);
+          has1 = true;
         }
         p = q + 1;
       }
     }
   }
-  if (!found) path = "/";
-  const std::string& root = v2 || !found ? root_v2 : root_v1;
-  int best = 0;
-  for (;;) {  // this cgroup, then each ancestor up to the mount root
-    const int c = cgroup_dir_cpus(root + (path == "/" ? "" : path), v2 || !found);
-    if (c > 0 && (best == 0 || c < best)) best = c;
-    if (path.empty() || path == "/") break;
-    const size_t s = path.find_last_of('/');
-    path = s == 0 || s == std::string::npos ? "/" : path.substr(0, s);
-  }
-  return best;
+  if (!has2 && !has1) return cgroup_walk_cpus(root_v2, "/", true);
+  const int c2 = has2 ? cgroup_walk_cpus(root_v2, p2, true) : 0;
+  const int c1 = has1 ? cgroup_walk_cpus(root_v1, p1, false) : 0;
+  return c2 > 0 && (c1 == 0 || c2 < c1) ? c2 : c1;
 }
 
 inline int usable_cpus_uncached() {

@@ -204,7 +204,7 @@ class Context:
         return out
 
     def time_sweep_batch(self, N, r, values, mask, times, scales, cost=None, status=None,
-                         asynchronous=False, split=False, dl=False, column=False):
+                         asynchronous=False, split=False, dl=False, column=False, general=False):
         dev = _is_torch(values) and values.is_cuda
         B, V, h, D = values.shape
         K = V - 1
@@ -228,6 +228,8 @@ class Context:
             flags |= nat.MTG_FLAG_DL_KERNEL
         if column:
             flags |= nat.MTG_FLAG_COLUMN_KERNEL
+        if general:
+            flags |= nat.MTG_FLAG_GENERAL_KERNEL
         rc = self._lib.mtg_time_sweep_batch(self.handle, N, D, K, r, B, _addr(values), _addr(mask),
                                             _addr(times), C, _addr(scales), _addr(cost), _addr(status), flags)
         nat.check(rc, self.handle)

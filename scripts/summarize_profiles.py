@@ -13,8 +13,10 @@ with 128-B requests).  Infinity-Cache (L3) hits are counted by these counters, s
 inputs stay L3-resident between launches this over-states true HBM bytes.
 
 usage: summarize_profiles.py TAG B [B ...]      (reads gpurun_out/prof<SRC>_b<B>, SRC from $PROF_SRC;
-       $WORKLOAD names the bench workload profiled, default config2: traffic is keyed
-       "<kernel>|<workload>" so a kernel profiled on one workload is not quoted for another)
+       $WORKLOAD names the bench workload profiled, default config2, and $PATTERN its vertex pattern
+       (bench.py --pattern), default generator: traffic is keyed "<kernel>|<workload>|<pattern>" and
+       stamped with the kernel sources' digest (bench.csrc_digest), so a capture is not quoted for
+       another workload, pattern or build)
 """
 import csv
 import json
@@ -63,6 +65,9 @@ def short(name):
 
 
 def main():
+    sys.path.insert(0, ROOT)
+    import bench
+    digest = bench.csrc_digest()
     tag = sys.argv[1]
     batches = sys.argv[2:]
     prof = os.path.join(ROOT, "profiles")
@@ -96,8 +101,10 @@ def main():
                 ent["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1.0)
             summary["kernels"][k] = ent
             if "hbm_bytes_per_launch" in ent and best.get(short(k)) == k:
-                key = "%s|%s" % (short(k), os.environ.get("WORKLOAD", "config2"))
+                key = bench.traffic_key(short(k), os.environ.get("WORKLOAD", "config2"),
+                                        os.environ.get("PATTERN", "generator"))
                 traffic.setdefault(key, {})[str(B)] = {
+                    "csrc_sha256": digest,
                     "hbm_bytes_per_launch": ent["hbm_bytes_per_launch"],
                     "fetch_kib_raw": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"],
                     "l2_hit_rate": ent.get("l2_hit_rate"), "profile": "%s_b%s_pmc.json" % (tag, B)}

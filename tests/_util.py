@@ -8,10 +8,10 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def golden_cases():
-    """The truth fixtures (tests/golden/make_golden.py); host_solve_bitwise.npz and
-    config4_truth_sample.npz are fixtures of their own (tests/golden/make_host_fixture.py,
-    tests/golden/make_config4_truth.py)."""
-    own = ("host_solve_bitwise.npz", "config4_truth_sample.npz")
+    """The truth fixtures (tests/golden/make_golden.py); host_solve_bitwise.npz, the truth samples
+    config4_truth_sample.npz / accel12_truth_sample.npz and offpattern_truth_n12.npz are fixtures of
+    their own (tests/golden/make_host_fixture.py, make_config4_truth.py, make_offpattern_truth.py)."""
+    own = ("host_solve_bitwise.npz", "config4_truth_sample.npz", "accel12_truth_sample.npz", "offpattern_truth_n12.npz")
     return sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
                   if os.path.basename(p) not in own)
 
@@ -117,3 +117,37 @@ def check_path(values, mask, times, coeffs, N, relative=False):
             cont = np.abs(end[:, :-1] - start[:, 1:]) / (scale if relative else 1.0)
             worst = max(worst, float(np.max(cont)))
     return worst
+
+
+def off_pattern_batch(N, D, K, B, seed0, kind):
+    """Batches whose masks are not the reference generators' pattern (the DL kernel's other passes):
+    "accel" / "jerk" are createRandomVertices with the ends fixed only to ACCELERATION / JERK (the
+    reference's 2_vertices_rand and ConstraintPacking masks, test/test_polynomial_optimization.cpp:747-774,
+    :777-836: the ends pass); "ends" pins random subsets of derivatives 1..N/2-1 at the two end
+    vertices only (ends pass); "random" pins derivatives 1..N/2-1 at random per vertex (values random)
+    and "vel" adds a fixed velocity at every interior vertex (the general-mask pass); "mixed" mixes the
+    pattern, "random", "ends" and a free interior position (the fallback)."""
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch, random_vertices_path_batch
+    h = N // 2
+    rng = np.random.default_rng(seed0)
+    if kind in ("accel", "jerk"):
+        md = min(2 if kind == "accel" else 3, h - 1)
+        return random_vertices_batch(N, D, K, B, [-50.0] * D, [50.0] * D, seed0=seed0, max_derivative=md)
+    vals, mask, times = random_vertices_path_batch(N, D, K, B, seed0=seed0, max_derivative=min(4, h - 1))
+    vals, mask = vals.copy(), mask.copy()
+    if kind == "vel":
+        mask[:, 1:-1] |= 2
+        vals[:, 1:-1, 1, :] = rng.normal(size=vals[:, 1:-1, 1, :].shape)
+    elif kind in ("random", "mixed", "ends"):
+        sel = rng.random(B) < (1.0 if kind == "random" else (0.5 if kind == "mixed" else 0.0))
+        pins = (rng.integers(0, 1 << h, size=(B, K + 1)) | 1).astype(np.uint8)
+        mask[sel] = pins[sel]
+        vals[sel, :, 1:, :] = rng.normal(size=vals[sel, :, 1:, :].shape)
+        ends = ~sel & (rng.random(B) < (1.0 if kind == "ends" else 0.5))
+        for v in (0, K):
+            mask[ends, v] = pins[ends, v]
+            vals[ends, v, 1:, :] = rng.normal(size=vals[ends, v, 1:, :].shape)
+        if kind == "mixed":
+            free_pos = rng.random(B) < 0.05
+            mask[free_pos, K // 2] &= np.uint8(0xFE)  # a free interior position: the fallback
+    return vals, mask, times

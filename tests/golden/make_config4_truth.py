@@ -1,12 +1,21 @@
 #!/usr/bin/env python3
-"""Fixture config4_truth_sample.npz: 60-digit truth (make_golden.truth_solve, the reference algorithm
-of polynomial_optimization_linear_impl.h:329-369 evaluated in mpmath) for a random sample of 256
-trajectories of the full-size config-4 batch (1e4 x N = 12, K = 20, JERK; the bench's generator,
-createRandomVertices(SNAP, 20, [-10,-20,-10], [10,20,10]) + estimateSegmentTimes(3, 5), seed0 = 0).
+"""Truth-sample fixtures: 60-digit truth (make_golden.truth_solve, the reference algorithm of
+polynomial_optimization_linear_impl.h:329-369 evaluated in mpmath) for a random sample of the
+trajectories of a full-size 1e4 batch.
 
-The GPU test regenerates the whole batch, solves all 1e4 on the default path and compares the sampled
+  config4 -> config4_truth_sample.npz: N = 12, K = 20, JERK; the bench's config-4 generator,
+             createRandomVertices(SNAP, 20, [-10,-20,-10], [10,20,10]) + estimateSegmentTimes(3, 5),
+             seed0 = 0; 256 trajectories (the DL kernel's long-chain pattern pass).
+  accel12 -> accel12_truth_sample.npz: N = 12, K = 20, JERK with the ends fixed only to ACCELERATION,
+             createRandomVertices(ACCELERATION, 20, [-50]^3, [50]^3) + estimateSegmentTimes(3, 5),
+             seed0 = 500; 96 trajectories (the ends pass: the reference's 2_vertices_rand pattern,
+             test/test_polynomial_optimization.cpp:747-774, on a long trajectory).
+
+The GPU tests regenerate the whole batch, solve all 1e4 on the default path and compare the sampled
 trajectories with this truth; the SHA-256 of the sampled inputs is stored so a generator change cannot
-pass silently.  About 7.6 s per trajectory: run here with 8 processes (~4 min)."""
+pass silently.  About 7.6 s per trajectory: run here with 8 processes (config4 ~4 min, accel12 ~1.5 min).
+
+  python tests/golden/make_config4_truth.py [config4|accel12]"""
 import hashlib
 import os
 import sys
@@ -20,15 +29,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 N, K, r, B, S = 12, 20, 3, 10000, 256
 
+CASES = {
+    "config4": dict(lo=[-10.0, -20.0, -10.0], hi=[10.0, 20.0, 10.0], seed0=0, max_derivative=4, S=256,
+                    sample_seed=20, file="config4_truth_sample.npz"),
+    "accel12": dict(lo=[-50.0] * 3, hi=[50.0] * 3, seed0=500, max_derivative=2, S=96, sample_seed=21,
+                    file="accel12_truth_sample.npz"),
+}
 
-def batch():
+
+def batch(case="config4"):
     from mav_trajectory_generation_cmake_amd import random_vertices_batch
-    return random_vertices_batch(N, 3, K, B, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=0,
-                                 max_derivative=4, v_max=3.0, a_max=5.0)
+    c = CASES[case]
+    return random_vertices_batch(N, 3, K, B, c["lo"], c["hi"], seed0=c["seed0"], max_derivative=c["max_derivative"],
+                                 v_max=3.0, a_max=5.0)
 
 
-def sample_index():
-    return np.sort(np.random.default_rng(20).choice(B, S, replace=False))
+def sample_index(case="config4"):
+    c = CASES[case]
+    return np.sort(np.random.default_rng(c["sample_seed"]).choice(B, c["S"], replace=False))
 
 
 def inputs_digest(vals, mask, times, idx):
@@ -43,15 +61,15 @@ def _one(args):
     return truth_solve(N, r, *args)[0]
 
 
-def main():
-    vals, mask, times = batch()
-    idx = sample_index()
+def main(case="config4"):
+    vals, mask, times = batch(case)
+    idx = sample_index(case)
     with Pool(int(os.environ.get("JOBS", "8"))) as p:
         tr = p.map(_one, [(vals[b], mask[b], times[b]) for b in idx], chunksize=1)
-    np.savez_compressed(os.path.join(HERE, "config4_truth_sample.npz"), index=idx,
+    np.savez_compressed(os.path.join(HERE, CASES[case]["file"]), index=idx,
                         coeffs=np.stack(tr).astype(np.float64),
                         inputs_sha256=np.array(inputs_digest(vals, mask, times, idx)))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "config4")

@@ -169,6 +169,7 @@ def test_cgroup_quota_walks_ancestors_and_v1(tmp_path):
     assert run("0::/kube/pod/ctr") == 16          # the parent's quota caps the nested cgroup
     assert run("0::/loose") == 2                  # its own quota (2.5 CPUs -> 2)
     assert run("0::/") == 0                       # namespace root without a quota
-    assert run("12:cpu,cpuacct:/a/b;0::/") == 0   # hybrid: the v2 line wins
+    assert run("12:cpu,cpuacct:/a/b;0::/") == 8   # hybrid: no v2 cpu.max, the v1 quota counts
+    assert run("12:cpu,cpuacct:/a/b;0::/loose") == 2  # hybrid with both quotas: the smaller
     assert run("12:cpu,cpuacct:/a/b") == 8        # v1: the ancestor's cfs quota
     assert run("3:memory:/x;5:cpuset:/y") == 0    # no cpu controller line
