@@ -53,8 +53,9 @@ def build(keep, unit, r, src):
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     name = "solve_dl_kernelILi%sELi%dELi" % (unit.split("_")[0][1:], r)
-    # the AL16 = true instantiation's body
-    m = re.search(r"^(_ZN3mtg15%s\w*Lb1E\w*):[^\n]*\n(.*?)^\.Lfunc_end" % name, asm, re.S | re.M)
+    # the instantiation with the 16-B aligned output and plain stores (AL16 = 1; POL env: 2, sc1 stores)
+    m = re.search(r"^(_ZN3mtg15%s\w*ELi%sEEEvNS_10DlKernArgsE):[^\n]*\n(.*?)^\.Lfunc_end"
+                  % (name, os.environ.get("POL", "1")), asm, re.S | re.M)
     body = m.group(2)
     lines = body.splitlines()
     isins = [bool(re.match(r"^\s+[a-z_][a-z0-9_.]*\b", l)) and not l.strip().startswith(".") for l in lines]
