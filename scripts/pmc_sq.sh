@@ -24,3 +24,4 @@ for grp in "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CY
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o run -- \
       python3 bench.py --steps 10 --warmup 2 --batch $B --no-cpu-baseline $EXTRA > $OUT/p$i.log 2>&1 || { echo "group $grp failed"; }
 done
+rm -f $OUT/p*/run_kernel_trace.csv

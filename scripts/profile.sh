@@ -17,3 +17,6 @@ run rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_wr
     python3 bench.py --steps 50 --warmup 200 --batch $B --no-cpu-baseline $EXTRA > $OUT/bench_write.log 2>&1 || exit $?
 run rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pmc_l2 -o run -- \
     python3 bench.py --steps 50 --warmup 200 --batch $B --no-cpu-baseline $EXTRA > $OUT/bench_l2.log 2>&1 || exit $?
+# (the per-dispatch kernel traces are not summarised -- the stats and counter files are: dropped so a
+# set of profiles fits gpurun_out)
+rm -f $OUT/trace/run_kernel_trace.csv $OUT/pmc_*/run_kernel_trace.csv
