@@ -488,10 +488,7 @@ __global__ __launch_bounds__(kScanThreads) void eval_scan_kernel(int64_t nb, int
 }
 
 // Runs per round of the LDS table (from the run table, or built by lane 0), consumed by the wave.
-#ifndef MTG_EVAL_RUNS
-#define MTG_EVAL_RUNS 32
-#endif
-constexpr int kRuns = MTG_EVAL_RUNS;
+constexpr int kRuns = 32;
 constexpr int kEvalThreads = 64;
 
 // (A run's length is the next run's n0 less its own.  Config 2, K = 10, D = 3, N = 10: this table
@@ -519,14 +516,9 @@ __device__ __forceinline__ bool stored_whole(const RunHead& h, int64_t n_total, 
 // registers of the sample loop only (the one-call evaluateRange; a second launch, ST = false with
 // `rest`, takes the others).
 constexpr int kSpl = 2;
-#ifndef MTG_EVAL_EXP
-#define MTG_EVAL_EXP 0  // (diagnostic builds only: 1 no run lookup, 2 no Horner, 3 stores dropped)
-#endif
-#ifndef MTG_EVAL_WAVES
-#define MTG_EVAL_WAVES 5
-#endif
+constexpr int kEvalWaves = 5;  // waves per SIMD the stored-run (ST) kernel's registers are built for
 template <int N, int DER, int DD, bool ST>
-__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST ? MTG_EVAL_WAVES : 4))) void eval_range_kernel(int D, int K, const double* coeffs,
+__global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST ? kEvalWaves : 4))) void eval_range_kernel(int D, int K, const double* coeffs,
                                                                   const double* times, double t_start, double t_end,
                                                                   double dt, int derivative, const int64_t* counts,
                                                                   const int64_t* offsets, double* out,
@@ -663,12 +655,10 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
         for (int s = 0; s < kSpl; ++s) {
           const int64_t n = nb + s * kEvalThreads + lane;
           const bool have = s * kEvalThreads + lane < cnt;
-#if MTG_EVAL_EXP != 1
           while (have && nxt <= n) {
             ++ri;
             nxt = ri + 1 < nr ? rt->n0[ri + 1] : INT64_MAX;
           }
-#endif
           const int64_t k = n - rt->n0[ri];
           double t, a;
           if (rt->single[ri]) {
@@ -678,15 +668,11 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
             t = mant_exp(rt->tm[ri] + k * rt->ti[ri], rt->tE[ri]);
             a = sample_times ? mant_exp(rt->am[ri] + k * rt->ai[ri], rt->aE[ri]) : 0.0;
           }
-#if MTG_EVAL_EXP == 1
-          t = (double)n * 1e-3;
-          a = t;
-#endif
           tv[s] = t;
           sg[s] = rt->seg[ri];
           cs[s] = cf + (sg[s] * DDc) * N;
           if (sample_times)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), rs, have && MTG_EVAL_EXP != 3 ? (uint32_t)(n * 8) : kBufOOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, a), rs, have ? (uint32_t)(n * 8) : kBufOOB, 0, 0);
         }
         double v[kSpl][DDc];
         // Usually the whole block lies in one segment (a segment has ~750 samples at dt = 0.01): its
@@ -697,14 +683,6 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
         bool same = true;
 #pragma unroll
         for (int s = 0; s < kSpl; ++s) same = same && sg[s] == sg0;
-#if MTG_EVAL_EXP == 2
-        if (true) {
-#pragma unroll
-          for (int s = 0; s < kSpl; ++s)
-#pragma unroll
-            for (int d = 0; d < DDc; ++d) v[s][d] = tv[s] + d;
-        } else
-#endif
         if (__builtin_amdgcn_ballot_w64(!same) == 0) {
           if (sg0 != cseg) {
             const double* c0 = cf + (sg0 * DDc) * N;
@@ -760,11 +738,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
 #pragma unroll
           for (int d = 0; d < DDc; ++d) ob[(s * kEvalThreads + lane) * DDc + d] = v[s][d];
         lds_fence();  // one wave per block: the staged rows are complete
-#if MTG_EVAL_EXP == 3
-        const uint32_t o0 = kBufOOB;
-#else
         const uint32_t o0 = (uint32_t)(nb * DDc * 8);  // the block's first row, bytes into the trajectory's rows
-#endif
         if (cnt == kBlk && al16) {  // whole 16-B pieces, 1 KiB per store instruction
           dvec2 w[P16];
 #pragma unroll
@@ -838,12 +812,7 @@ __global__ __launch_bounds__(kEvalThreads) __attribute__((amdgpu_waves_per_eu(ST
 // compute; the kernel took ~0.63 ms where its compute alone took ~0.39 and its stores alone ~0.44.
 // The two waves meet at one s_barrier per block; the barrier waits only for LDS (the store wave's
 // global stores stay in flight).  Samples, rows and their order are the one-wave kernel's exactly.
-#ifndef MTG_EVAL_PC
-#define MTG_EVAL_PC 1
-#endif
-#ifndef MTG_EVAL_PC_WAVES
-#define MTG_EVAL_PC_WAVES 5
-#endif
+constexpr int kEvalPcWaves = 5;  // waves per SIMD the producer / consumer kernel is built for
 struct PcSlot {
   double v[kSpl * kEvalThreads * 3];  // the block's rows, sample-major
   double ts[kSpl * kEvalThreads];     // its sample times
@@ -857,7 +826,7 @@ static_assert(sizeof(PcSlot) % 16 == 0, "slots stay 16-B aligned");
 __device__ __forceinline__ void pc_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int N, int DER>
-__global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_eu(MTG_EVAL_PC_WAVES))) void eval_range_pc_kernel(
+__global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_eu(kEvalPcWaves))) void eval_range_pc_kernel(
     int K, const double* coeffs, int derivative, const int64_t* counts, const int64_t* offsets, double* out,
     double* sample_times, int cap, const RunHead* heads, const RunRec* runs, const int64_t* boff,
     int64_t* offsets_out, int64_t capacity, const int64_t* total) {
@@ -896,11 +865,7 @@ __global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_e
       double tv[kSpl];
 #pragma unroll
       for (int q = 0; q < kSpl; ++q) tv[q] = sl->ts[q * kEvalThreads + lane];
-#if MTG_EVAL_EXP == 3
-      const uint32_t o0 = kBufOOB;  // (diagnostic builds: every store dropped)
-#else
       const uint32_t o0 = (uint32_t)(nb * DD * 8);
-#endif
       if (cnt == kBlk && al16) {
         dvec2 w[P16];
 #pragma unroll
@@ -923,7 +888,7 @@ __global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
         for (int q = 0; q < kSpl; ++q)
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, tv[q]), rs,
-                                                q * kEvalThreads + lane < cnt && MTG_EVAL_EXP != 3 ? (uint32_t)((nb + q * kEvalThreads + lane) * 8) : kBufOOB, 0, 0);
+                                                q * kEvalThreads + lane < cnt ? (uint32_t)((nb + q * kEvalThreads + lane) * 8) : kBufOOB, 0, 0);
       }
     }
     return;
@@ -990,14 +955,6 @@ __global__ __launch_bounds__(2 * kEvalThreads) __attribute__((amdgpu_waves_per_e
       bool same = true;
 #pragma unroll
       for (int q = 0; q < kSpl; ++q) same = same && sg[q] == sg0;
-#if MTG_EVAL_EXP == 2
-      if (true) {  // (diagnostic builds: no Horner)
-#pragma unroll
-        for (int q = 0; q < kSpl; ++q)
-#pragma unroll
-          for (int d = 0; d < DD; ++d) v[q][d] = tv[q] + d;
-      } else
-#endif
       if (__builtin_amdgcn_ballot_w64(!same) == 0) {
         if (sg0 != cseg) {
           const double* c0 = cf + (sg0 * DD) * N;
@@ -1154,15 +1111,12 @@ hipError_t launch_eval_range(int N, int D, int K, int64_t B, const double* coeff
   const size_t lds = sizeof(RunLds) + sizeof(double) * ((size_t)K * D * N + (size_t)(d3 ? kSpl : 1) * kEvalThreads * D);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   const size_t lds_pc = sizeof(RunLds) + sizeof(double) * (size_t)K * 3 * N + 2 * sizeof(PcSlot);
-  const bool pc = MTG_EVAL_PC && lds_pc <= 64 * 1024;  // (else the one-wave kernel)
+  const bool pc = lds_pc <= 64 * 1024;  // (else the one-wave kernel)
   const dim3 grid((unsigned)B);
   // D = 3 with the run table: a stored-run launch takes every trajectory whose whole clock is in it
   // (the producer / consumer kernel, or the one-wave ST kernel when its LDS would not fit), and the
   // run-time-D kernel (rest) the others -- its blocks for the stored ones return at once
-#ifndef MTG_EVAL_STORED
-#define MTG_EVAL_STORED 1  // (0: one launch of the D = 3 kernel with the lane-0 clock, for A/B builds)
-#endif
-  const bool stored = MTG_EVAL_STORED && heads != nullptr && d3;
+  const bool stored = heads != nullptr && d3;
 #define MTG_EVAL_LAUNCH(NN, DER)                                                                                   \
   do {                                                                                                             \
     if (stored && pc) {                                                                                            \
