@@ -1491,3 +1491,31 @@ def test_dl_general_masks_dropped_orders_and_not_spd(gpu_ctx, N, K, r, kind):
     c = gpu_ctx.solve_linear_batch(N, r, vals, mask, t2, status=True)
     assert c["status"][3] & nat.MTG_TRAJ_NOT_SPD
     assert np.all(c["status"][np.arange(B) != 3] == 0)
+
+
+@pytest.mark.parametrize("N,K,r,B_big", [(10, 10, 4, 30000), (12, 20, 3, 35000)])
+def test_store_policy_does_not_change_results(gpu_ctx, N, K, r, B_big):
+    """The DL kernel writes its coefficients with the sc1 cache policy while the launch's output stays
+    in the Infinity Cache and with plain stores above (mtg_solve_dl.inc dl_store_sc1: 64 MB for the
+    short chains, 192 MB for the long ones).  A batch above the limit (plain stores) and its first
+    1e4 trajectories alone (sc1) give the same coefficients, free values and status, bit for bit."""
+    from mav_trajectory_generation_cmake_amd import random_vertices_batch, random_vertices_path_batch
+    D = 3
+    if N == 10:
+        vals, mask, times = random_vertices_path_batch(N, D, K, B_big, seed0=123)
+    else:
+        vals, mask, times = random_vertices_batch(N, D, K, B_big, [-10.0, -20.0, -10.0], [10.0, 20.0, 10.0], seed0=123,
+                                                  max_derivative=4, v_max=3.0, a_max=5.0)
+    import torch
+    limit = (64 if N == 10 else 192) << 20
+    assert B_big * K * D * N * 8 > limit and 10000 * K * D * N * 8 <= limit
+    # device arrays: one launch per call (host arrays above 8 MB run as a pipeline of smaller chunks)
+    dev = torch.device("cuda:0")
+    dv, dm, dt = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (vals, mask, times))
+    kw = dict(free=True, status=True)
+    big = gpu_ctx.solve_linear_batch(N, r, dv, dm, dt, **kw)
+    small = gpu_ctx.solve_linear_batch(N, r, dv[:10000], dm[:10000], dt[:10000], **kw)
+    torch.cuda.synchronize()
+    assert np.all(big["status"].cpu().numpy() == 0)
+    for k in ("coeffs", "free", "status"):
+        np.testing.assert_array_equal(small[k].cpu().numpy(), big[k][:10000].cpu().numpy(), err_msg=k)
