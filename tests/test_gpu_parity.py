@@ -1519,3 +1519,25 @@ def test_store_policy_does_not_change_results(gpu_ctx, N, K, r, B_big):
     assert np.all(big["status"].cpu().numpy() == 0)
     for k in ("coeffs", "free", "status"):
         np.testing.assert_array_equal(small[k].cpu().numpy(), big[k][:10000].cpu().numpy(), err_msg=k)
+
+
+@pytest.mark.parametrize("N,D,K,r", [(10, 3, 10, 4), (12, 3, 20, 3)])
+def test_dl_passes_output_alignment(gpu_ctx, N, D, K, r):
+    """Every pass of the DL kernel (pattern, ends, general-mask, fallback: a "mixed" batch) writes the
+    same coefficients into an output that is only 8-B aligned (the AL16 = 0 instantiation: 8-B
+    pieces) as into a 16-B aligned one, bit for bit."""
+    import torch
+    B = 300
+    vals, mask, times = _off_pattern_batch(N, D, K, B, 4711 + N, "mixed")
+    dev = torch.device("cuda:0")
+    dv, dm, dt = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (vals, mask, times))
+    shape = (B, K, D, N)
+    c16 = torch.zeros(shape, dtype=torch.float64, device=dev)
+    buf = torch.zeros(B * K * D * N + 1, dtype=torch.float64, device=dev)
+    c8 = buf[1:].view(shape)
+    gpu_ctx.solve_linear_batch(N, r, dv, dm, dt, coeffs=c16)
+    gpu_ctx.solve_linear_batch(N, r, dv, dm, dt, coeffs=c8)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c8.cpu().numpy(), c16.cpu().numpy())
+    host = gpu_ctx.solve_linear_batch(N, r, vals, mask, times)["coeffs"]
+    np.testing.assert_array_equal(c16.cpu().numpy(), host)
