@@ -105,6 +105,11 @@ extern "C" {
 #define MTG_KERNEL_GENERAL 3           /* general LDS-resident fused kernel (any K) */
 #define MTG_KERNEL_SPLIT 4             /* assembly kernel + block-Cholesky kernel */
 #define MTG_KERNEL_DL 6                /* one lane per (chain, dimension) (MTG_FLAG_DL_KERNEL) */
+#define MTG_KERNEL_DLX 7               /* the same for chains of other lengths (N = 10 / 12, D <= 4, r >= 1,
+                                          where neither the DL nor the column kernel applies: e.g. the
+                                          reference benchmark's K = 50 / 100), plus the general kernel's
+                                          block function for trajectories whose interior vertices do not
+                                          fix exactly their position */
 
 typedef struct mtg_ctx mtg_ctx;
 

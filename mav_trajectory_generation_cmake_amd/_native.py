@@ -39,9 +39,10 @@ MTG_KERNEL_COLUMN = 2
 MTG_KERNEL_GENERAL = 3
 MTG_KERNEL_SPLIT = 4
 MTG_KERNEL_DL = 6
+MTG_KERNEL_DLX = 7
 KERNEL_NAMES = {MTG_KERNEL_COLUMN: "solve_reg_kernel",
                 MTG_KERNEL_GENERAL: "solve_fused_kernel", MTG_KERNEL_SPLIT: "assemble+block_cholesky",
-                MTG_KERNEL_DL: "solve_dl_kernel"}
+                MTG_KERNEL_DL: "solve_dl_kernel", MTG_KERNEL_DLX: "solve_dlx_kernel"}
 
 _c_dp = ctypes.c_void_p  # every array argument is passed as a raw address
 

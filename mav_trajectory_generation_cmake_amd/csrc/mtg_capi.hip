@@ -366,6 +366,11 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
   const size_t o_nfree = off; off = align_up(off + s_nfree * chunk);
   const size_t o_cost = off; off = align_up(off + s_cost * chunk);
   const size_t o_status = off; off = align_up(off + s_status * chunk);
+  // the long-chain DL kernel's workspace, per slot (the slots' kernels may run at once)
+  const unsigned ksel = kflags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
+  const size_t s_work = mtg::solve_kernel(N, D, K, ksel, r, chunk) == MTG_KERNEL_DLX
+                            ? mtg::dlx_workspace_bytes(N, D, K, chunk) : 0;
+  const size_t o_work = off; off = align_up(off + s_work);
   MTG_HIP_TRY(ctx, ensure_pipe(ctx));
   for (auto& s : ctx->pipe) MTG_HIP_TRY(ctx, ensure(&s.dev, &s.dev_bytes, off));
 
@@ -460,6 +465,8 @@ int run_solve_pipelined(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch,
       a.n_free_out = n_free_out ? reinterpret_cast<int32_t*>(dp + o_nfree) : nullptr;
       a.cost_out = cost_out ? reinterpret_cast<double*>(dp + o_cost) : nullptr;
       a.status = status ? reinterpret_cast<int32_t*>(dp + o_status) : nullptr;
+      a.work = s_work ? reinterpret_cast<double*>(dp + o_work) : nullptr;
+      a.work_bytes = (int64_t)s_work;
       e = mtg::launch_solve(N, a, s.stream, kflags);
     }
     if (e == hipSuccess) e = hipEventRecord(s.k_done, s.stream);
@@ -500,8 +507,8 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     // the explicit flag keeps it so)
     const unsigned kf = flags & (MTG_FLAG_GENERAL_KERNEL |
                                  MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
-    const unsigned pin = mtg::solve_kernel(N, D, K, kf, r, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
-                                                                                     : MTG_FLAG_COLUMN_KERNEL;
+    const int kk = mtg::solve_kernel(N, D, K, kf, r, batch);
+    const unsigned pin = (kk == MTG_KERNEL_DL || kk == MTG_KERNEL_DLX) ? MTG_FLAG_DL_KERNEL : MTG_FLAG_COLUMN_KERNEL;
     const int rc = run_solve_pipelined(ctx, N, D, K, r, batch, values, mask, times, coeffs, free_out, n_free_out,
                                        cost_out, status, kf | pin);
     if (rc != kPipelineUnavailable) return rc;
@@ -598,13 +605,21 @@ int run_solve(mtg_ctx* ctx, int N, int D, int K, int r, int64_t batch, const dou
     // entries beyond n_free are left zero
     MTG_HIP_TRY(ctx, hipMemsetAsync(const_cast<double*>(a.free_out), 0, b_free, ctx->stream));
   }
-  MTG_HIP_TRY(ctx, time_begin(ctx, !(flags & MTG_FLAG_SPLIT_KERNELS)));
+  const unsigned ksel = flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL);
+  const bool dlx = !(flags & MTG_FLAG_SPLIT_KERNELS) && mtg::solve_kernel(N, D, K, ksel, r, pairs) == MTG_KERNEL_DLX;
+  if (dlx) {  // the long-chain DL kernel's workspace (and two launches: the timed region spans both)
+    const size_t wb = mtg::dlx_workspace_bytes(N, D, K, pairs);
+    MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(wb, 256)));
+    a.work = static_cast<double*>(ctx->workspace);
+    a.work_bytes = (int64_t)ctx->workspace_bytes;
+  }
+  MTG_HIP_TRY(ctx, time_begin(ctx, !(flags & MTG_FLAG_SPLIT_KERNELS) && !dlx));
   if (flags & MTG_FLAG_SPLIT_KERNELS) {
     const size_t ws = mtg::split_workspace_bytes(N, D, K, pairs);
     MTG_HIP_TRY(ctx, ensure(&ctx->workspace, &ctx->workspace_bytes, std::max<size_t>(ws, 256)));
     MTG_HIP_TRY(ctx, mtg::launch_solve_split(N, a, ctx->workspace, ctx->stream));
   } else {
-    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, flags & (MTG_FLAG_GENERAL_KERNEL | MTG_FLAG_DL_KERNEL | MTG_FLAG_COLUMN_KERNEL)));
+    MTG_HIP_TRY(ctx, mtg::launch_solve(N, a, ctx->stream, ksel));
   }
   MTG_HIP_TRY(ctx, time_end(ctx));
   if (pin) {
@@ -802,8 +817,10 @@ int mtg_solve_linear_batch_multi(mtg_ctx* const* ctxs, int n_ctxs, int N, int D,
   // the batch size -- the DL kernel for N = 10 / K = 10 and N = 12 / K = 20 at every size -- but the
   // flag keeps the choice explicit), so the result does not depend on the number of devices
   if (!(flags & MTG_FLAG_SPLIT_KERNELS))
-    flags |= mtg::solve_kernel(N, D, K, flags, derivative_to_optimize, batch) == MTG_KERNEL_DL ? MTG_FLAG_DL_KERNEL
-                                                                                             : MTG_FLAG_COLUMN_KERNEL;
+  {
+    const int kk = mtg::solve_kernel(N, D, K, flags, derivative_to_optimize, batch);
+    flags |= (kk == MTG_KERNEL_DL || kk == MTG_KERNEL_DLX) ? MTG_FLAG_DL_KERNEL : MTG_FLAG_COLUMN_KERNEL;
+  }
   auto shard = [&](int g) {
     int64_t b0 = 0, b1 = 0;
     mtg_shard_range(batch, n_ctxs, g, &b0, &b1);

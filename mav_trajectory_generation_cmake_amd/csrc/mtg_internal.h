@@ -47,6 +47,8 @@ struct SolveArgs {
   int n_cand;             // candidates per trajectory for the sweep (1 for a plain solve)
   int gi;                 // register column kernel: G in LDS for the interior-waypoint body (set by
                           // launch_solve_reg, mtg_solve_reg.inc reg_gi_doubles)
+  double* work;           // long-chain dimension-lane kernel: its workspace (dlx_workspace_bytes)
+  int64_t work_bytes;
 };
 
 // Lanes per trajectory and LDS bytes per workgroup for a shape; returns false
@@ -67,6 +69,11 @@ hipError_t launch_solve_reg(int N, const SolveArgs& a, hipStream_t stream);
 // derivative, interior vertices exactly their position): one lane per (chain, dimension)
 bool dl_geometry(int N, int D, int K, int r);
 hipError_t launch_solve_dl(int N, const SolveArgs& a, hipStream_t stream);
+// the same recurrence for chains of any length (mtg_solve_dlx.hip), where neither the DL kernel nor
+// the column kernel applies; its workspace (a.work) holds dlx_workspace_bytes for the launch's batch
+bool dlx_geometry(int N, int D, int K, int r);
+size_t dlx_workspace_bytes(int N, int D, int K, int64_t B);
+hipError_t launch_solve_dlx(int N, const SolveArgs& a, hipStream_t stream);
 
 // Two-kernel path (MTG_FLAG_SPLIT_KERNELS): assembly into the block-tridiagonal
 // workspace, then the block-Cholesky solve + recovery.

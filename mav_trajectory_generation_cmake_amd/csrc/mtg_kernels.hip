@@ -116,6 +116,9 @@ int solve_kernel(int N, int D, int K, unsigned flags, int r, int64_t B) {
   const bool dl_default = !(flags & MTG_FLAG_COLUMN_KERNEL);
   if (((flags & MTG_FLAG_DL_KERNEL) || dl_default) && r >= 0 && dl_geometry(N, D, K, r)) return MTG_KERNEL_DL;
   if (reg_geometry(N, D, K, &lg, &lds)) return MTG_KERNEL_COLUMN;
+  // chains of other lengths: the long-chain dimension-lane kernel (with the general kernel's block
+  // function for the trajectories it does not serve)
+  if (((flags & MTG_FLAG_DL_KERNEL) || dl_default) && r >= 0 && dlx_geometry(N, D, K, r)) return MTG_KERNEL_DLX;
   return MTG_KERNEL_GENERAL;
 }
 
@@ -123,6 +126,7 @@ hipError_t launch_solve(int N, const SolveArgs& a, hipStream_t stream, unsigned 
   switch (solve_kernel(N, a.D, a.K, flags, a.r, a.B)) {
     case MTG_KERNEL_DL: return launch_solve_dl(N, a, stream);
     case MTG_KERNEL_COLUMN: return launch_solve_reg(N, a, stream);
+    case MTG_KERNEL_DLX: return launch_solve_dlx(N, a, stream);  // (a.work: the caller's)
     default: break;
   }
   switch (N) {

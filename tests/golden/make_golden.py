@@ -105,6 +105,52 @@ def truth_solve(N, r, vals, mask, times):
     return coeffs, float(cost / 2), free_out, fixed_out
 
 
+def truth_solve_banded(N, r, vals, mask, times):
+    """truth_solve's coefficients for long chains: the same 60-digit system (_system), R_pp solved by a
+    banded LDL^T elimination (R_pp is block tridiagonal in the reference's (vertex, derivative) order,
+    SPD, so no pivoting) instead of a dense LU -- O(n bw^2) instead of O(n^3) multiprecision operations
+    (N = 10, K = 64: ~1 s instead of ~80 s).  Same digits: the tests use it where truth_solve is too
+    slow (tests/test_oracle.py checks the two agree)."""
+    h = N // 2
+    V, nd, D = vals.shape
+    K = V - 1
+    R, fixed, free, col, Ainvs, Qs = _system(N, r, vals, mask, times)
+    nf, npf = len(fixed), len(free)
+    A = [[R[nf + a][nf + b] for b in range(npf)] for a in range(npf)]
+    bw = 0
+    for a in range(npf):
+        for b in range(a + 1, npf):
+            if A[a][b] != 0:
+                bw = max(bw, b - a)
+    for i in range(npf):  # in-place LDL^T (unit L below the diagonal, pivots on it)
+        piv = A[i][i]
+        for j in range(i + 1, min(npf, i + bw + 1)):
+            f = A[i][j] / piv  # (the upper triangle is the updated one)
+            if f == 0:
+                continue
+            for k in range(j, min(npf, i + bw + 1)):
+                A[j][k] -= f * A[i][k]
+            A[j][i] = f
+    coeffs = np.zeros((K, D, N))
+    for d in range(D):
+        df = [mp.mpf(float(vals[v, k, d])) for (v, k) in fixed]
+        x = [-mp.fsum(R[nf + a][b] * df[b] for b in range(nf)) for a in range(npf)]
+        for i in range(npf):
+            for j in range(i + 1, min(npf, i + bw + 1)):
+                x[j] -= A[j][i] * x[i]
+        for i in range(npf - 1, -1, -1):
+            t = x[i] / A[i][i]
+            for j in range(i + 1, min(npf, i + bw + 1)):
+                t -= A[j][i] * x[j]
+            x[i] = t
+        dall = df + x
+        for i in range(K):
+            cols = [col[(i + (s >= h), s % h)] for s in range(N)]
+            c = Ainvs[i] * mp.matrix([dall[c] for c in cols])
+            coeffs[i, d] = [float(c[j]) for j in range(N)]
+    return coeffs
+
+
 def fp64_best_solve(N, r, vals, mask, times):
     """What a backward-stable FP64 solve reaches on this problem: R_pp and the right-hand side formed
     exactly (60 digits) and rounded once to FP64, equilibrated (symmetric diagonal scaling), solved

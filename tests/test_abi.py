@@ -119,8 +119,8 @@ def test_cpp_header_compiles_with_c_compiler(tmp_path):
 
 def test_solve_kernel_selection():
     """mtg_solve_kernel (host-only query): the register column kernel by default for K <= 12 (N = 12:
-    K <= 20), the dimension-lane kernel with MTG_FLAG_DL_KERNEL where it applies, the general kernel
-    beyond, errors for rejected shapes; the retired lane / IP flag bits (16, 32) are ignored."""
+    K <= 20), the dimension-lane kernel with MTG_FLAG_DL_KERNEL where it applies, the long-chain
+    dimension-lane kernel or the general kernel beyond, errors for rejected shapes; the retired lane / IP flag bits (16, 32) are ignored."""
     from mav_trajectory_generation_cmake_amd import _native as nat
     lib = nat.load()
     dl, col, gen, split = (nat.MTG_KERNEL_DL, nat.MTG_KERNEL_COLUMN, nat.MTG_KERNEL_GENERAL,
@@ -142,10 +142,24 @@ def test_solve_kernel_selection():
         assert lib.mtg_solve_kernel(10, 3, 10, 4, retired) == nat.MTG_KERNEL_DL
     assert lib.mtg_solve_kernel(12, 3, 20, 3, L) == dl
     assert lib.mtg_solve_kernel(12, 5, 20, 3, L) == col  # D > 4
-    assert lib.mtg_solve_kernel(10, 3, 12, 4, 0) == gen   # G of 6 vertices exceeds both register budgets
+    # K outside both the DL kernel's (10 / 20) and the column kernel's (N = 10: <= 10) ranges: the
+    # long-chain DL kernel (round 6) where it applies (N = 10 / 12, D <= 4, r >= 1), else the general one
+    dlx = nat.MTG_KERNEL_DLX
+    assert lib.mtg_solve_kernel(10, 3, 12, 4, 0) == dlx
+    assert lib.mtg_solve_kernel(10, 3, 11, 4, 0) == dlx
+    assert lib.mtg_solve_kernel(10, 3, 100, 4, 0) == dlx  # the reference benchmark's K = 100
+    assert lib.mtg_solve_kernel(10, 1, 101, 1, 0) == dlx
+    assert lib.mtg_solve_kernel(12, 4, 21, 3, 0) == dlx
+    assert lib.mtg_solve_kernel(10, 3, 50, 4, L) == dlx
+    assert lib.mtg_solve_kernel(10, 3, 50, 4, nat.MTG_FLAG_COLUMN_KERNEL) == gen  # (no column kernel there)
+    assert lib.mtg_solve_kernel(10, 3, 50, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
+    assert lib.mtg_solve_kernel(10, 3, 50, 0, 0) == gen   # r = 0
+    assert lib.mtg_solve_kernel(10, 5, 50, 4, 0) == gen   # D > 4
+    assert lib.mtg_solve_kernel(8, 3, 50, 3, 0) == gen    # N = 8
+    assert nat.solve_kernel(10, 3, 50, 4) == "solve_dlx_kernel"
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_SPLIT_KERNELS) == split
-    assert lib.mtg_solve_kernel(10, 3, 13, 4, 0) == gen
+    assert lib.mtg_solve_kernel(10, 3, 13, 4, 0) == dlx
     # the dimension-lane kernel by default wherever it applies (N = 10, K = 10, D <= 4, r >= 1), at
     # every batch size (a trajectory's bits do not depend on the size of its call); the column flag
     # keeps the column kernel
@@ -160,7 +174,7 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel_batch(12, 3, 20, 3, 125000, 0) == dl
     assert lib.mtg_solve_kernel_batch(10, 3, 10, 4, 125000, nat.MTG_FLAG_SPLIT_KERNELS) == split
     assert nat.solve_kernel(10, 3, 10, 4, B=125000) == "solve_dl_kernel"
-    assert lib.mtg_solve_kernel(10, 3, 50, 4, 0) == gen
+    assert lib.mtg_solve_kernel(10, 3, 50, 4, 0) == nat.MTG_KERNEL_DLX
     assert lib.mtg_solve_kernel(11, 3, 10, 4, 0) == nat.MTG_ERR_UNSUPPORTED_N
     assert lib.mtg_solve_kernel(10, 3, 10, 5, 0) == nat.MTG_ERR_BAD_DERIVATIVE
     assert nat.solve_kernel(10, 3, 10, 4) == "solve_dl_kernel"

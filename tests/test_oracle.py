@@ -109,6 +109,22 @@ def test_oracle_vs_truth(case):
         assert abs(res["cost"] - g["cost"][b]) <= 1e-5 * abs(g["cost"][b]) + 1e-12
 
 
+def test_truth_banded_matches_dense_truth():
+    """make_golden.truth_solve_banded (the 60-digit reference system solved by banded LDL^T, the long-K
+    arbiter of tests/test_gpu_dlx.py) reproduces the committed dense-LU truth fixtures: the first two
+    trajectories of every fixture (K up to 50, N = 6..12, every mask kind), exactly after rounding."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_golden import truth_solve_banded
+    for case in golden_cases():
+        g = load_golden(case)
+        N, r = int(g["N"]), int(g["r"])
+        for b in range(min(2, len(g["times"]))):
+            vals, mask = to_abi(g["values"][b:b + 1], g["mask"][b:b + 1], N)
+            c = truth_solve_banded(N, r, vals[0], mask[0], g["times"][b])
+            err = scale_normalised_error(c[None], g["coeffs"][b][None], g["times"][b][None])
+            assert err <= 1e-15, (case, b, err)
+
+
 def _setup(N, r, vals, mask, times):
     res = O.solve_linear(N, r, vals, mask, times, want_matrices=True)
     K = len(times)
