@@ -488,7 +488,9 @@ def main():
     total = units * world * args.steps
     value = total / el
     achieved = bpt * B / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = traffic_from_profiles(kname, B, wl, args.pattern)
+    # (a capture is keyed by the workload's shape: "config2-K100" for config 2's generator at K = 100)
+    wl_key = wl if (args.N is None and args.segments is None) else "%s-N%dK%d" % (wl, N, K)
+    traffic, traffic_src = traffic_from_profiles(kname, B, wl_key, args.pattern)
     out = {
         "metric": metric,
         "value": value,

@@ -1,6 +1,7 @@
 # Round-6 closing run, part A: the -m gpu suite, smoke, and the bench lines --
 # config 2 (the headline, default and the driver's 20/5), the config-3 shard, config 4, config 5,
-# the off-pattern batches, evaluateRange and the extrema.  The first crash or timeout ends it.
+# the off-pattern batches, the reference benchmark's long chains (K = 50 / 100, the long-chain DL
+# kernel; K = 100 on the general kernel beside it), evaluateRange and the extrema.  The first crash or timeout ends it.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${EVID:-r06z}
@@ -23,9 +24,12 @@ b bench_c2_vel --pattern interior-vel --no-cpu-baseline --no-end-to-end
 b bench_c2_vel_column --pattern interior-vel --column-kernel --no-cpu-baseline --no-end-to-end
 b bench_c4_accel --workload config4 --pattern accel-ends --no-cpu-baseline --no-end-to-end
 b bench_c4_accel_column --workload config4 --pattern accel-ends --column-kernel --no-cpu-baseline --no-end-to-end
+b bench_k50 --segments 50 --no-cpu-baseline --no-end-to-end
+b bench_k100 --segments 100 --steps 200 --no-cpu-baseline --no-end-to-end
+b bench_k100_general --segments 100 --steps 50 --warmup 20 --general-kernel --no-cpu-baseline --no-end-to-end
 timeout -k 10 200 python scripts/bench_eval.py > $O/bench_eval.json 2> $O/bench_eval.err || { tail $O/bench_eval.err; exit 1; }
 timeout -k 10 200 python scripts/bench_extrema.py > $O/bench_extrema.json 2> $O/bench_extrema.err || { tail $O/bench_extrema.err; exit 1; }
-for f in bench_c2 bench_20_5 bench_c3 bench_c4 bench_c5 bench_c2_accel bench_c2_accel_column bench_c2_vel bench_c2_vel_column bench_c4_accel bench_c4_accel_column; do
+for f in bench_c2 bench_20_5 bench_c3 bench_c4 bench_c5 bench_c2_accel bench_c2_accel_column bench_c2_vel bench_c2_vel_column bench_c4_accel bench_c4_accel_column bench_k50 bench_k100 bench_k100_general; do
   python -c "import json; d=json.load(open('$O/$f.json')); r=d['roofline']; print('$f', '%.4g' % d['value'], r['kernel'], 'kernel_ms %.4f' % r['kernel_ms'], 'frac %.3f' % r['frac'])"
 done
 echo OK > $O/done
