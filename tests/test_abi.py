@@ -155,7 +155,10 @@ def test_solve_kernel_selection():
     assert lib.mtg_solve_kernel(10, 3, 50, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 50, 0, 0) == gen   # r = 0
     assert lib.mtg_solve_kernel(10, 5, 50, 4, 0) == gen   # D > 4
-    assert lib.mtg_solve_kernel(8, 3, 50, 3, 0) == gen    # N = 8
+    assert lib.mtg_solve_kernel(8, 3, 50, 3, 0) == dlx    # N = 8 / 6 beyond the column kernel's K <= 12
+    assert lib.mtg_solve_kernel(6, 2, 13, 2, 0) == dlx
+    assert lib.mtg_solve_kernel(8, 3, 12, 3, 0) == col
+    assert lib.mtg_solve_kernel(4, 3, 50, 1, 0) == gen    # N = 4: the general kernel
     assert nat.solve_kernel(10, 3, 50, 4) == "solve_dlx_kernel"
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_GENERAL_KERNEL) == gen
     assert lib.mtg_solve_kernel(10, 3, 10, 4, nat.MTG_FLAG_SPLIT_KERNELS) == split

@@ -1,4 +1,4 @@
-"""The long-chain dimension-lane kernel (round 6, mtg_solve_dlx.inc): N = 10 / 12
+"""The long-chain dimension-lane kernel (round 6, mtg_solve_dlx.inc): N = 6..12
 trajectories whose K has no fixed-length DL kernel and no column kernel -- the reference benchmark's
 K = 50 and 100 (src/polynomial_timing_evaluation.cpp:117) among them.
 
@@ -139,7 +139,8 @@ def _vs_oracle_and_truth(N, r, vals, mask, times, coeffs, S, T=3):
 
 
 SHAPES = [(10, 3, 50, 4), (10, 3, 100, 4), (10, 3, 11, 4), (10, 3, 13, 4), (10, 1, 50, 2), (10, 4, 37, 3),
-          (10, 2, 64, 4), (10, 3, 12, 1), (12, 3, 21, 3), (12, 3, 40, 3), (12, 4, 33, 2), (12, 1, 25, 4)]
+          (10, 2, 64, 4), (10, 3, 12, 1), (12, 3, 21, 3), (12, 3, 40, 3), (12, 4, 33, 2), (12, 1, 25, 4),
+          (8, 3, 30, 3), (8, 2, 13, 2), (8, 4, 51, 1), (6, 3, 40, 2), (6, 1, 17, 1)]
 
 
 @pytest.mark.parametrize("N,D,K,r", SHAPES)
@@ -165,7 +166,8 @@ def test_dlx_pattern_vs_general_and_oracle(gpu_ctx, N, D, K, r):
 @pytest.mark.parametrize("N,D,K,r,kind", [(10, 3, 50, 4, "accel"), (10, 3, 50, 4, "jerk"), (10, 3, 50, 4, "ends"),
                                           (10, 3, 50, 4, "mixed"), (10, 3, 50, 4, "vel"), (10, 3, 50, 4, "random"),
                                           (10, 3, 17, 4, "mixed"), (10, 1, 23, 2, "ends"), (12, 3, 30, 3, "accel"),
-                                          (12, 4, 30, 3, "mixed"), (12, 3, 21, 3, "ends")])
+                                          (12, 4, 30, 3, "mixed"), (12, 3, 21, 3, "ends"), (8, 3, 30, 3, "accel"),
+                                          (8, 3, 25, 3, "mixed"), (6, 2, 20, 2, "ends")])
 def test_dlx_other_masks(gpu_ctx, N, D, K, r, kind):
     """Masks other than the generators' pattern: ends fixed only to ACCELERATION / JERK (2_vertices_rand,
     ConstraintPacking, test/test_polynomial_optimization.cpp:747-836) and random end pins -- DLX's
