@@ -29,7 +29,10 @@ b bench_k100 --segments 100 --steps 200 --no-cpu-baseline --no-end-to-end
 b bench_k100_general --segments 100 --steps 50 --warmup 20 --general-kernel --no-cpu-baseline --no-end-to-end
 timeout -k 10 200 python scripts/bench_eval.py > $O/bench_eval.json 2> $O/bench_eval.err || { tail $O/bench_eval.err; exit 1; }
 timeout -k 10 200 python scripts/bench_extrema.py > $O/bench_extrema.json 2> $O/bench_extrema.err || { tail $O/bench_extrema.err; exit 1; }
+timeout -k 10 300 python scripts/bench_dlx_shapes.py > $O/bench_dlx_shapes.jsonl 2> $O/bench_dlx_shapes.err || { tail $O/bench_dlx_shapes.err; exit 1; }
+timeout -k 10 300 python scripts/timing_eval.py > $O/latency_table.jsonl 2> $O/latency_table.err || { tail $O/latency_table.err; exit 1; }
 for f in bench_c2 bench_20_5 bench_c3 bench_c4 bench_c5 bench_c2_accel bench_c2_accel_column bench_c2_vel bench_c2_vel_column bench_c4_accel bench_c4_accel_column bench_k50 bench_k100 bench_k100_general; do
   python -c "import json; d=json.load(open('$O/$f.json')); r=d['roofline']; print('$f', '%.4g' % d['value'], r['kernel'], 'kernel_ms %.4f' % r['kernel_ms'], 'frac %.3f' % r['frac'])"
 done
+cat $O/bench_dlx_shapes.jsonl
 echo OK > $O/done
