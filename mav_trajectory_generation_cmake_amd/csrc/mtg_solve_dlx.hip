@@ -40,7 +40,8 @@ static int64_t dlx_rec_doubles(int N, int D) {
 }
 
 // Workspace of one launch over B trajectories (pairs): one wave slot per resident wave, at most one per
-// wave of work; each slot KB = K - K/2 records.
+// wave of work, each slot KB = K - K/2 records; then one 32-bit word per wave of work (which of its
+// trajectories the rest kernel solves).
 size_t dlx_workspace_bytes(int N, int D, int K, int64_t B) {
   if (B <= 0 || !dlx_geometry(N, D, K, 1)) return 0;
   int64_t resident = 0;
@@ -55,7 +56,8 @@ size_t dlx_workspace_bytes(int N, int D, int K, int64_t B) {
   if (resident <= 0 || tpw <= 0) return 0;
   const int64_t tasks = (B + tpw - 1) / tpw;
   const int64_t slots = tasks < resident ? tasks : resident;
-  return (size_t)slots * (size_t)(K - K / 2) * (size_t)dlx_rec_doubles(N, D) * sizeof(double);
+  const size_t rest = (size_t)((tasks * 4 + 255) / 256 * 256);  // the per-wave rest bits, at the end
+  return (size_t)slots * (size_t)(K - K / 2) * (size_t)dlx_rec_doubles(N, D) * sizeof(double) + rest;
 }
 
 hipError_t launch_solve_dlx(int N, const SolveArgs& a, hipStream_t stream) {

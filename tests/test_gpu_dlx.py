@@ -42,7 +42,7 @@ def nat_traj_bad_time():
 
 
 def _served(mask, K):
-    """Trajectories the DLX kernel itself solves (dlx_vertex_ok on every vertex)."""
+    """Trajectories the DLX kernel itself solves: interior masks exactly 1 (the position), end masks with bit 0."""
     ends = (mask[:, 0] & 1).astype(bool) & (mask[:, K] & 1).astype(bool)
     interior = np.all(mask[:, 1:K] == 1, axis=1) if K > 1 else np.ones(len(mask), bool)
     return ends & interior
